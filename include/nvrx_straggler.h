@@ -1,0 +1,200 @@
+/*
+ * nvrx_straggler.h -- C ABI of the MI355X-native straggler-detection scoring path.
+ *
+ * Implemented by libnvrx_hip.so (hand-written HIP kernels for gfx950).  Every entry
+ * point takes plain pointers and sizes; no torch types cross this boundary.  Device
+ * pointers are caller-owned (e.g. torch tensors' data_ptr()); `stream` is a
+ * hipStream_t (NULL = default stream).  Calls are stream-ordered and asynchronous,
+ * except nvrx_sync, the nvrx_profiler_* lifecycle calls and functions documented as
+ * "synchronous".  Nothing is retained after return except state owned by a
+ * nvrx_profiler handle.
+ *
+ * Errors: every function returns NVRX_OK (0) or a negative NVRX_ERR_*; the message
+ * of the last error on the calling thread is nvrx_last_error().  The Python layer
+ * raises RuntimeError with that message, as the reference's CUPTI_CALL -> std::
+ * runtime_error -> RuntimeError path does (cupti_src/CuptiProfiler.cpp:30-38).
+ *
+ * Reference interfaces replaced (paths relative to
+ * /root/reference/src/nvidia_resiliency_ext/straggler):
+ *   nvrx_segment_stats_*   computeStats + CuptiProfiler::getStats   cupti_src/CuptiProfiler.cpp:44-74, 136-146
+ *   nvrx_kernel_ref        ReportGenerator._all_reduce_times (MIN over ranks, -1 => NaN)   reporting.py:255-296
+ *   nvrx_pack_min_times    the [K+Nsec] float32 pack of _all_reduce_times                 reporting.py:269-279
+ *   nvrx_scores            _update_local_min_times + _compute_gpu_perf_score              reporting.py:298-314, 219-253
+ *   nvrx_finalize_scores   score = sum(s*w)/sum(w), NaN if no common kernel; optional
+ *                          float32 rounding of _get_tensor_from_scores                    reporting.py:251-253, 338-361
+ *   nvrx_section_scores    _compute_sections_perf_scores (+ section MIN reduce, history)  reporting.py:196-217, 255-314
+ *   nvrx_stragglers        Report.identify_stragglers (score < threshold, strict)         reporting.py:84-151
+ *   nvrx_profiler_*        nvrx_cupti_module.CuptiProfiler (ctor, initialize, shutdown,
+ *                          start, stop, get_stats, reset)                                 cupti_src/cupti_module_py.cpp:33-54
+ *   nvrx_records_*         CuptiProfiler::bufferCompleted record loop + CircularBuffer     cupti_src/CuptiProfiler.cpp:168-203, CircularBuffer.h:53-69
+ */
+#ifndef NVRX_STRAGGLER_H
+#define NVRX_STRAGGLER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NVRX_ABI_VERSION 1
+
+#define NVRX_OK 0
+#define NVRX_ERR_INVALID -1   /* bad argument / shape */
+#define NVRX_ERR_HIP -2       /* HIP runtime error */
+#define NVRX_ERR_STATE -3     /* call not valid in the current state */
+#define NVRX_ERR_SINGLETON -4 /* a second profiler instance (CuptiProfiler.cpp:86-87) */
+#define NVRX_ERR_NOMEM -5
+
+/* statistics modes */
+#define NVRX_STATS_FAST 0  /* NUM/MIN/MAX/MED bit-exact; AVG/STD exact mean/std rounded once to f32 */
+#define NVRX_STATS_EXACT 1 /* every field bit-exact with computeStats (sequential f32 over sorted) */
+
+/* largest retained segment (statsMaxLenPerKernel) the kernels accept */
+#define NVRX_MAX_SEGMENT 32768
+
+/* SoA output of the statistics kernels: one entry per segment (device pointers).
+ * Units are microseconds as float32, like KernelStats (CuptiProfiler.h:39-45). */
+typedef struct nvrx_stats_soa {
+    int32_t* num;
+    float* min;
+    float* max;
+    float* med;
+    float* avg;
+    float* std;
+} nvrx_stats_soa;
+
+/* Arguments of nvrx_scores: R score rows (ranks) x K kernel columns, row-major. */
+typedef struct nvrx_score_args {
+    int64_t R, K;
+    const int32_t* num;        /* [R][K] NUM; <= 0 means the kernel is absent on that rank */
+    const float* med;          /* [R][K] MED (us) */
+    const float* avg;          /* [R][K] AVG (us) */
+    const uint8_t* col_valid;  /* [K] 0 = column filtered out ("ncclDev"), NULL = all valid */
+    /* relative score reference (NULL = relative scores not computed) */
+    const float* ref;          /* ref[ref_index ? ref_index[k] : k]; a value !(>= 0) (NaN, -1) = missing */
+    const int32_t* ref_index;  /* [K] or NULL */
+    /* individual score history (NULL = individual scores not computed); updated in place
+     * to min(hist, MED) for every present kernel BEFORE scoring (reporting.py:469-474) */
+    float* hist;               /* hist[r*hist_stride + (hist_index ? hist_index[k] : k)] */
+    const int32_t* hist_index; /* [K] or NULL */
+    int64_t hist_stride;       /* per-row stride of hist; 0 => K */
+    /* output: partial sums per row, 6 doubles:
+     * {sum s*w (rel), sum w (rel), n (rel), sum s*w (ind), sum w (ind), n (ind)} */
+    double* partials;          /* [R][6] */
+    int32_t* err;              /* [1] device flags |= 1 when some MED == 0 (ZeroDivisionError) */
+} nvrx_score_args;
+
+/* ---------------------------------------------------------------- library */
+const char* nvrx_last_error(void);
+int nvrx_abi_version(void);
+int nvrx_device_count(int* count);             /* synchronous */
+int nvrx_sync(void* stream);                   /* synchronous: waits for `stream` */
+
+/* ---------------------------------------------------------------- statistics */
+/* Segment s = ns[s*seg_stride + seg_begin : + seg_len] (uint32 ns durations); the
+ * last min(seg_len, cap) samples are retained (cap <= 0: all).  out->* are [nseg]. */
+int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
+                               int64_t seg_begin, int64_t seg_len, int64_t cap, int32_t mode,
+                               const nvrx_stats_soa* out, void* stream);
+/* Segment s = ns[seg_off[s] : seg_off[s] + seg_len[s]] (device arrays; seg_len NULL:
+ * seg_off has nseg+1 entries and segment s ends at seg_off[s+1]); max_len bounds every
+ * segment length (host-known); aligned16 != 0 promises every retained run starts on a
+ * 16-byte boundary. */
+int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
+                              int64_t nseg, int64_t max_len, int64_t cap, int32_t mode,
+                              int32_t aligned16, const nvrx_stats_soa* out, void* stream);
+
+/* ---------------------------------------------------------------- scoring */
+/* ref[k] = min over r of med[r][k] if num[r][k] > 0 for every r, else NaN.
+ * scratch: >= 2*K uint32 of device memory. */
+int nvrx_kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
+                    uint32_t* scratch, void* stream);
+/* times[0:total] = -1; times[ids[i]] = (float)med_f32[i] (i < nk), then
+ * times[ids_sec[j]] = (float)med_f64[j] (j < nsec): the _all_reduce_times pack. */
+int nvrx_pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
+                        const double* med_f64, const int32_t* ids_sec, int64_t nsec,
+                        float* times, int64_t total, void* stream);
+int nvrx_scores(const nvrx_score_args* args, void* stream);
+/* partials: [nshards][R][6], combined in shard order 0..nshards-1.
+ * score = n > 0 ? sum(s*w)/sum(w) : NaN; round_f32 != 0 rounds to float32 (the
+ * gather_on_rank0 tensor); err |= 2 when n > 0 and sum(w) == 0.
+ * Any output pointer may be NULL. strag_* = score < thr (strict; NaN never). */
+int nvrx_finalize_scores(const double* partials, int64_t R, int64_t nshards, int32_t round_f32,
+                         double thr_rel, double thr_ind, double* gpu_rel, double* gpu_ind,
+                         uint8_t* strag_rel, uint8_t* strag_ind, int32_t* err, void* stream);
+/* Sections, R rows x S sections: med [R][S] f64, present [R][S] u8.
+ * rel: ref_s = min over rows of float32(med) when ref_in == NULL (every row must be
+ *      present, else NaN; computed into ref_work [S]), or ref_in[ref_index ? ref_index[s] : s]
+ *      (float32, !(>= 0) = missing => NaN score);
+ * ind: hist[R][S] f64 updated to min(hist, med) first.
+ * out_rel / out_ind [R][S] f64 (NaN where absent); round_f32 as above.  Either may be NULL;
+ * err |= 1 when a present med == 0 (ZeroDivisionError). */
+int nvrx_section_scores(const double* med, const uint8_t* present, int64_t R, int64_t S,
+                        const float* ref_in, const int32_t* ref_index, float* ref_work,
+                        double* hist, int32_t round_f32, double* out_rel, double* out_ind,
+                        int32_t* err, void* stream);
+int nvrx_stragglers(const double* score, int64_t n, double thr, uint8_t* mask, void* stream);
+
+/* ---------------------------------------------------------------- record streams */
+/* A record is one kernel execution: the slot of its composite kernel name and its
+ * duration in ns (end - start, CuptiProfiler.cpp:187; clamped to UINT32_MAX). */
+typedef struct nvrx_record {
+    uint32_t slot;
+    uint32_t ns;
+} nvrx_record;
+
+/* Bucket nstreams push-ordered record streams (stream t = recs[rec_off[t] : rec_off[t+1]],
+ * one per rank) by slot, keeping for every (stream, slot) only its LAST `cap` records
+ * (CircularBuffer semantics; order inside a bucket is push order).  Outputs (device):
+ *   seg_off [nstreams*nslots] int64, seg_len [nstreams*nslots] int32:
+ *       bucket (t, s) = out_ns[seg_off[t*nslots+s] : + seg_len[t*nslots+s]]; every bucket
+ *       starts 16-byte aligned, so it feeds nvrx_segment_stats_ragged(aligned16=1)
+ *   out_ns  [>= nvrx_records_bucket_capacity(n, nstreams, nslots)] uint32
+ *   counts  [nstreams*nslots] int32: total pushes per (stream, slot) on return */
+int64_t nvrx_records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots);
+int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                        int64_t nslots, int64_t cap, int64_t* seg_off, int32_t* seg_len,
+                        uint32_t* out_ns, int32_t* counts, void* stream);
+/* Largest nslots nvrx_records_bucket accepts (per-slot counters live in LDS). */
+int64_t nvrx_records_max_slots(void);
+
+/* ---------------------------------------------------------------- profiler handle */
+/* Replacement of nvrx_cupti_module.CuptiProfiler: owns device-resident per-kernel
+ * duration records; only one instance may exist (CuptiProfiler.cpp:83-90). */
+typedef struct nvrx_profiler nvrx_profiler;
+
+typedef struct nvrx_profiler_config {
+    int64_t buffer_size;              /* bytes of host record buffer per flush (CUPTI bufferSize) */
+    int64_t num_buffers;              /* CUPTI numBuffers (kept for API parity) */
+    int64_t stats_max_len_per_kernel; /* ring capacity per kernel (statsMaxLenPerKernel) */
+    int32_t device;                   /* HIP device ordinal */
+    int32_t mode;                     /* NVRX_STATS_EXACT (default) or NVRX_STATS_FAST */
+} nvrx_profiler_config;
+
+int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out);
+int nvrx_profiler_destroy(nvrx_profiler* p);
+int nvrx_profiler_initialize(nvrx_profiler* p);
+int nvrx_profiler_shutdown(nvrx_profiler* p);
+int nvrx_profiler_start(nvrx_profiler* p);
+int nvrx_profiler_stop(nvrx_profiler* p);
+int nvrx_profiler_reset(nvrx_profiler* p);
+/* Register a composite kernel name ("%s_blk_%d_%d_%d_grid_%d_%d_%d") -> slot. */
+int nvrx_profiler_register_kernel(nvrx_profiler* p, const char* name, uint32_t* slot);
+/* Append host records (push order).  Ignored while stopped (records are dropped). */
+int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n);
+/* Flush, then compute stats of every slot with >= 1 record.  Synchronous.
+ * Returns the number of kernels in *count; fills up to `cap_out` entries of slots
+ * (sorted by kernel name, as std::map in getStats) and host SoA outputs. */
+int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
+                            int32_t* num, float* mn, float* mx, float* med, float* avg,
+                            float* sd);
+int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_t buflen);
+/* Live kernel-dispatch capture through rocprofiler-sdk (0 = not available). */
+int nvrx_profiler_capture_available(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* NVRX_STRAGGLER_H */

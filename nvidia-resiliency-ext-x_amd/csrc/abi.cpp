@@ -1,0 +1,538 @@
+// abi.cpp -- the extern "C" boundary of libnvrx_hip.so (declared in include/nvrx_straggler.h).
+//
+// Thin host glue: argument/shape checks on the host before any launch, HIP error ->
+// status code + thread-local message, and the profiler handle that replaces the
+// reference's nvrx_cupti_module.CuptiProfiler (straggler/cupti_src/CuptiProfiler.cpp,
+// cupti_module_py.cpp).  All arithmetic runs in the HIP kernels of segment_stats.hip,
+// scores.hip and records.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nvrx_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+int hip_status(hipError_t e, const char* where) {
+    if (e == hipSuccess) return NVRX_OK;
+    return fail(e == hipErrorInvalidValue ? NVRX_ERR_INVALID : NVRX_ERR_HIP,
+                std::string(where) + ": " + hipGetErrorString(e));
+}
+#define NVRX_CHECK_ARG(cond, msg) \
+    do {                          \
+        if (!(cond)) return fail(NVRX_ERR_INVALID, msg); \
+    } while (0)
+
+hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+const char* nvrx_last_error(void) { return g_last_error.c_str(); }
+int nvrx_abi_version(void) { return NVRX_ABI_VERSION; }
+
+int nvrx_device_count(int* count) {
+    NVRX_CHECK_ARG(count, "nvrx_device_count: null count");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e == hipErrorNoDevice) c = 0, e = hipSuccess;
+    *count = c;
+    return hip_status(e, "hipGetDeviceCount");
+}
+
+int nvrx_sync(void* stream) { return hip_status(hipStreamSynchronize(S(stream)), "nvrx_sync"); }
+
+// ------------------------------------------------------------------ statistics
+int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
+                               int64_t seg_begin, int64_t seg_len, int64_t cap, int32_t mode,
+                               const nvrx_stats_soa* out, void* stream) {
+    NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
+                   "nvrx_segment_stats_strided: null output array");
+    NVRX_CHECK_ARG(nseg >= 0 && seg_len >= 0 && seg_begin >= 0 && seg_stride >= 0,
+                   "nvrx_segment_stats_strided: negative size");
+    NVRX_CHECK_ARG(nseg == 0 || seg_len == 0 || ns, "nvrx_segment_stats_strided: null ns");
+    NVRX_CHECK_ARG(mode == NVRX_STATS_FAST || mode == NVRX_STATS_EXACT,
+                   "nvrx_segment_stats_strided: unknown mode");
+    NVRX_CHECK_ARG(nseg <= 1 || seg_stride >= seg_begin + seg_len,
+                   "nvrx_segment_stats_strided: segments overlap (stride < begin + len)");
+    const int64_t keep = (cap > 0 && seg_len > cap) ? cap : seg_len;
+    NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT,
+                   "nvrx_segment_stats_strided: retained segment longer than NVRX_MAX_SEGMENT");
+    NVRX_CHECK_ARG(nseg < (int64_t)1 << 33, "nvrx_segment_stats_strided: too many segments");
+    return hip_status(nvrx::segment_stats_strided(ns, nseg, seg_stride, seg_begin, seg_len, cap,
+                                                  mode, *out, S(stream)),
+                      "nvrx_segment_stats_strided");
+}
+
+int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
+                              int64_t nseg, int64_t max_len, int64_t cap, int32_t mode,
+                              int32_t aligned16, const nvrx_stats_soa* out, void* stream) {
+    NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
+                   "nvrx_segment_stats_ragged: null output array");
+    NVRX_CHECK_ARG(nseg >= 0 && max_len >= 0, "nvrx_segment_stats_ragged: negative size");
+    NVRX_CHECK_ARG(nseg == 0 || (seg_off && ns), "nvrx_segment_stats_ragged: null input");
+    NVRX_CHECK_ARG(mode == NVRX_STATS_FAST || mode == NVRX_STATS_EXACT,
+                   "nvrx_segment_stats_ragged: unknown mode");
+    const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
+    NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT,
+                   "nvrx_segment_stats_ragged: retained segment longer than NVRX_MAX_SEGMENT");
+    NVRX_CHECK_ARG(nseg < (int64_t)1 << 31, "nvrx_segment_stats_ragged: too many segments");
+    return hip_status(nvrx::segment_stats_ragged(ns, seg_off, seg_len, nseg, max_len, cap, mode,
+                                                 aligned16 != 0, *out, S(stream)),
+                      "nvrx_segment_stats_ragged");
+}
+
+// ------------------------------------------------------------------ scoring
+int nvrx_kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
+                    uint32_t* scratch, void* stream) {
+    NVRX_CHECK_ARG(R >= 0 && K >= 0, "nvrx_kernel_ref: negative size");
+    NVRX_CHECK_ARG(K == 0 || (ref && scratch), "nvrx_kernel_ref: null ref/scratch");
+    NVRX_CHECK_ARG(R == 0 || K == 0 || (num && med), "nvrx_kernel_ref: null num/med");
+    NVRX_CHECK_ARG((R + 63) / 64 < 65536, "nvrx_kernel_ref: too many rows");
+    return hip_status(nvrx::kernel_ref(num, med, R, K, ref, scratch, S(stream)), "nvrx_kernel_ref");
+}
+
+int nvrx_pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
+                        const double* med_f64, const int32_t* ids_sec, int64_t nsec,
+                        float* times, int64_t total, void* stream) {
+    NVRX_CHECK_ARG(nk >= 0 && nsec >= 0 && total >= 0, "nvrx_pack_min_times: negative size");
+    NVRX_CHECK_ARG(total == 0 || times, "nvrx_pack_min_times: null times");
+    NVRX_CHECK_ARG(nk == 0 || (med_f32 && ids), "nvrx_pack_min_times: null kernel inputs");
+    NVRX_CHECK_ARG(nsec == 0 || (med_f64 && ids_sec), "nvrx_pack_min_times: null section inputs");
+    NVRX_CHECK_ARG(nk + nsec <= total, "nvrx_pack_min_times: more entries than the tensor holds");
+    return hip_status(nvrx::pack_min_times(med_f32, ids, nk, med_f64, ids_sec, nsec, times, total,
+                                           S(stream)),
+                      "nvrx_pack_min_times");
+}
+
+int nvrx_scores(const nvrx_score_args* a, void* stream) {
+    NVRX_CHECK_ARG(a, "nvrx_scores: null args");
+    NVRX_CHECK_ARG(a->R >= 0 && a->K >= 0, "nvrx_scores: negative size");
+    NVRX_CHECK_ARG(a->R == 0 || a->partials, "nvrx_scores: null partials");
+    NVRX_CHECK_ARG(a->R == 0 || a->K == 0 || (a->num && a->med && a->avg),
+                   "nvrx_scores: null num/med/avg");
+    NVRX_CHECK_ARG(!a->hist_index || a->hist_stride > 0,
+                   "nvrx_scores: hist_index requires hist_stride");
+    return hip_status(nvrx::scores(*a, S(stream)), "nvrx_scores");
+}
+
+int nvrx_finalize_scores(const double* partials, int64_t R, int64_t nshards, int32_t round_f32,
+                         double thr_rel, double thr_ind, double* gpu_rel, double* gpu_ind,
+                         uint8_t* strag_rel, uint8_t* strag_ind, int32_t* err, void* stream) {
+    NVRX_CHECK_ARG(R >= 0 && nshards >= 1, "nvrx_finalize_scores: bad size");
+    NVRX_CHECK_ARG(R == 0 || partials, "nvrx_finalize_scores: null partials");
+    return hip_status(nvrx::finalize_scores(partials, R, nshards, round_f32, thr_rel, thr_ind,
+                                            gpu_rel, gpu_ind, strag_rel, strag_ind, err, S(stream)),
+                      "nvrx_finalize_scores");
+}
+
+int nvrx_section_scores(const double* med, const uint8_t* present, int64_t R, int64_t S_,
+                        const float* ref_in, const int32_t* ref_index, float* ref_work,
+                        double* hist, int32_t round_f32, double* out_rel, double* out_ind,
+                        int32_t* err, void* stream) {
+    NVRX_CHECK_ARG(R >= 0 && S_ >= 0, "nvrx_section_scores: negative size");
+    NVRX_CHECK_ARG(R == 0 || S_ == 0 || (med && present), "nvrx_section_scores: null med/present");
+    NVRX_CHECK_ARG(!out_ind || hist, "nvrx_section_scores: individual scores need hist");
+    NVRX_CHECK_ARG(!out_rel || ref_in || ref_work, "nvrx_section_scores: need ref_in or ref_work");
+    return hip_status(nvrx::section_scores(med, present, R, S_, ref_in, ref_index, ref_work, hist,
+                                           round_f32, out_rel, out_ind, err, S(stream)),
+                      "nvrx_section_scores");
+}
+
+int nvrx_stragglers(const double* score, int64_t n, double thr, uint8_t* mask, void* stream) {
+    NVRX_CHECK_ARG(n >= 0 && (n == 0 || (score && mask)), "nvrx_stragglers: bad args");
+    return hip_status(nvrx::stragglers(score, n, thr, mask, S(stream)), "nvrx_stragglers");
+}
+
+// ------------------------------------------------------------------ record streams
+int64_t nvrx_records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
+    return nvrx::records_bucket_capacity(n, nstreams, nslots);
+}
+int64_t nvrx_records_max_slots(void) { return NVRX_RECORDS_MAX_LDS / (3 * sizeof(uint32_t)); }
+
+int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                        int64_t nslots, int64_t cap, int64_t* seg_off, int32_t* seg_len,
+                        uint32_t* out_ns, int32_t* counts, void* stream) {
+    NVRX_CHECK_ARG(nstreams >= 0 && nslots >= 0, "nvrx_records_bucket: negative size");
+    NVRX_CHECK_ARG(nslots <= nvrx_records_max_slots(), "nvrx_records_bucket: too many slots");
+    NVRX_CHECK_ARG(nstreams == 0 || nslots == 0 ||
+                       (rec_off && seg_off && seg_len && out_ns && counts),
+                   "nvrx_records_bucket: null array");
+    NVRX_CHECK_ARG(nstreams < (int64_t)1 << 31, "nvrx_records_bucket: too many streams");
+    return hip_status(nvrx::records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off,
+                                           seg_len, out_ns, counts, S(stream)),
+                      "nvrx_records_bucket");
+}
+
+}  // extern "C"
+
+// ====================================================================== profiler handle
+struct nvrx_profiler {
+    nvrx_profiler_config cfg{};
+    std::mutex mu;
+    bool initialized = false;
+    bool started = false;
+    std::unordered_map<std::string, uint32_t> name_to_slot;
+    std::vector<std::string> names;
+    std::vector<nvrx_record> staged;  // host records not yet flushed to the device log
+    hipStream_t stream = nullptr;
+    // device record log (push order since the last reset)
+    nvrx_record* d_log = nullptr;
+    int64_t log_n = 0, log_cap = 0;
+    // work buffers (grown on demand)
+    void* d_work = nullptr;
+    size_t work_bytes = 0;
+};
+
+namespace {
+
+std::mutex g_instance_mu;
+nvrx_profiler* g_instance = nullptr;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int grow_log(nvrx_profiler* p, int64_t need) {
+    if (need <= p->log_cap) return NVRX_OK;
+    int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1 << 16, p->log_cap * 2));
+    nvrx_record* nl = nullptr;
+    hipError_t e = hipMalloc(&nl, (size_t)cap * sizeof(nvrx_record));
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler: hipMalloc(record log)");
+    if (p->log_n > 0) {
+        e = hipMemcpyAsync(nl, p->d_log, (size_t)p->log_n * sizeof(nvrx_record),
+                           hipMemcpyDeviceToDevice, p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(nl);
+            return hip_status(e, "nvrx_profiler: grow record log");
+        }
+    }
+    if (p->d_log) (void)hipFree(p->d_log);
+    p->d_log = nl;
+    p->log_cap = cap;
+    return NVRX_OK;
+}
+
+int ensure_work(nvrx_profiler* p, size_t bytes) {
+    if (bytes <= p->work_bytes) return NVRX_OK;
+    if (p->d_work) (void)hipFree(p->d_work);
+    p->d_work = nullptr;
+    p->work_bytes = 0;
+    size_t b = std::max(bytes, p->work_bytes * 2);
+    hipError_t e = hipMalloc(&p->d_work, b);
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler: hipMalloc(work)");
+    p->work_bytes = b;
+    return NVRX_OK;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Work {  // carve of d_work for one bucket + stats pass over the record log
+    int64_t* rec_off;
+    int64_t* seg_off;
+    int32_t* seg_len;
+    int32_t* counts;
+    uint32_t* ns;
+    int32_t* num;
+    float *mn, *mx, *med, *avg, *sd;
+    int64_t* dst_off;
+    size_t bytes;
+};
+
+Work carve(char* base, int64_t nslots, int64_t ns_cap) {
+    Work w{};
+    size_t o = 0;
+    auto take = [&](size_t b) {
+        char* p = base ? base + o : nullptr;
+        o += align256(b);
+        return p;
+    };
+    w.rec_off = (int64_t*)take(2 * sizeof(int64_t));
+    w.seg_off = (int64_t*)take(nslots * sizeof(int64_t));
+    w.seg_len = (int32_t*)take(nslots * sizeof(int32_t));
+    w.counts = (int32_t*)take(nslots * sizeof(int32_t));
+    w.ns = (uint32_t*)take(ns_cap * sizeof(uint32_t));
+    w.num = (int32_t*)take(nslots * sizeof(int32_t));
+    w.mn = (float*)take(nslots * sizeof(float));
+    w.mx = (float*)take(nslots * sizeof(float));
+    w.med = (float*)take(nslots * sizeof(float));
+    w.avg = (float*)take(nslots * sizeof(float));
+    w.sd = (float*)take(nslots * sizeof(float));
+    w.dst_off = (int64_t*)take(nslots * sizeof(int64_t));
+    w.bytes = o;
+    return w;
+}
+
+// Bucket the whole device log (one stream).  Caller holds p->mu.
+int bucket_log(nvrx_profiler* p, int64_t nslots, int force_stable, Work& w) {
+    const int64_t ns_cap = nvrx::records_bucket_capacity(p->log_n, 1, nslots);
+    Work probe = carve(nullptr, nslots, ns_cap);
+    int rc = ensure_work(p, probe.bytes);
+    if (rc) return rc;
+    w = carve((char*)p->d_work, nslots, ns_cap);
+    int64_t off[2] = {0, p->log_n};
+    hipError_t e = hipMemcpyAsync(w.rec_off, off, sizeof(off), hipMemcpyHostToDevice, p->stream);
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler: rec_off upload");
+    e = nvrx::records_bucket(p->d_log, w.rec_off, 1, nslots, p->cfg.stats_max_len_per_kernel,
+                             force_stable, w.seg_off, w.seg_len, w.ns, w.counts, p->stream);
+    return hip_status(e, "nvrx_profiler: records_bucket");
+}
+
+// Flush staged host records into the device log; compact the log when it is much
+// larger than what the rings can retain.  Caller holds p->mu.
+int flush_locked(nvrx_profiler* p) {
+    DeviceGuard g(p->cfg.device);
+    if (!p->staged.empty()) {
+        const int64_t add = (int64_t)p->staged.size();
+        int rc = grow_log(p, p->log_n + add);
+        if (rc) return rc;
+        hipError_t e = hipMemcpyAsync(p->d_log + p->log_n, p->staged.data(),
+                                      (size_t)add * sizeof(nvrx_record), hipMemcpyHostToDevice,
+                                      p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+        if (e != hipSuccess) return hip_status(e, "nvrx_profiler: flush");
+        p->log_n += add;
+        p->staged.clear();
+    }
+    const int64_t nslots = (int64_t)p->names.size();
+    const int64_t cap = p->cfg.stats_max_len_per_kernel;
+    const int64_t retain_bound = nslots * (cap > 0 ? cap : p->log_n);
+    if (cap > 0 && p->log_n > (int64_t)1 << 22 && p->log_n > 4 * retain_bound &&
+        nslots <= nvrx_records_max_slots()) {
+        // compaction keeps exactly the records a later retention step could still keep
+        Work w;
+        int rc = bucket_log(p, nslots, /*force_stable=*/1, w);
+        if (rc) return rc;
+        std::vector<int32_t> len(nslots);
+        hipError_t e = hipMemcpyAsync(len.data(), w.seg_len, nslots * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+        if (e != hipSuccess) return hip_status(e, "nvrx_profiler: compaction lengths");
+        std::vector<int64_t> dst(nslots);
+        int64_t tot = 0;
+        for (int64_t s = 0; s < nslots; ++s) dst[s] = tot, tot += len[s];
+        nvrx_record* nl = nullptr;
+        e = hipMalloc(&nl, (size_t)std::max<int64_t>(tot, 1) * sizeof(nvrx_record));
+        if (e != hipSuccess) return hip_status(e, "nvrx_profiler: hipMalloc(compaction)");
+        e = hipMemcpyAsync(w.dst_off, dst.data(), nslots * sizeof(int64_t), hipMemcpyHostToDevice,
+                           p->stream);
+        if (e == hipSuccess)
+            e = nvrx::records_unbucket(w.seg_off, w.seg_len, w.dst_off, w.ns, nslots, nl, p->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(nl);
+            return hip_status(e, "nvrx_profiler: compaction");
+        }
+        (void)hipFree(p->d_log);
+        p->d_log = nl;
+        p->log_n = tot;
+        p->log_cap = std::max<int64_t>(tot, 1);
+    }
+    return NVRX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
+    NVRX_CHECK_ARG(cfg && out, "nvrx_profiler_create: null argument");
+    NVRX_CHECK_ARG(cfg->stats_max_len_per_kernel > 0 &&
+                       cfg->stats_max_len_per_kernel <= NVRX_MAX_SEGMENT,
+                   "nvrx_profiler_create: statsMaxLenPerKernel must be in [1, NVRX_MAX_SEGMENT]");
+    NVRX_CHECK_ARG(cfg->mode == NVRX_STATS_FAST || cfg->mode == NVRX_STATS_EXACT,
+                   "nvrx_profiler_create: unknown mode");
+    std::lock_guard<std::mutex> lk(g_instance_mu);
+    if (g_instance)  // CuptiProfiler.cpp:86-87
+        return fail(NVRX_ERR_SINGLETON, "Only one CuptiProfiler instance is allowed.");
+    auto* p = new nvrx_profiler();
+    p->cfg = *cfg;
+    {
+        DeviceGuard g(cfg->device);
+        hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete p;
+            return hip_status(e, "nvrx_profiler_create: hipStreamCreate");
+        }
+    }
+    g_instance = p;
+    *out = p;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_destroy(nvrx_profiler* p) {
+    NVRX_CHECK_ARG(p, "nvrx_profiler_destroy: null handle");
+    {
+        std::lock_guard<std::mutex> lk(g_instance_mu);
+        if (g_instance == p) g_instance = nullptr;
+    }
+    {
+        DeviceGuard g(p->cfg.device);
+        if (p->d_log) (void)hipFree(p->d_log);
+        if (p->d_work) (void)hipFree(p->d_work);
+        if (p->stream) (void)hipStreamDestroy(p->stream);
+    }
+    delete p;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_initialize(nvrx_profiler* p) {
+    NVRX_CHECK_ARG(p, "nvrx_profiler_initialize: null handle");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->initialized)
+        std::fprintf(stderr, "CuptiProfiler::initializeProfiling subsequent call.\n");
+    p->initialized = true;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_shutdown(nvrx_profiler* p) {
+    NVRX_CHECK_ARG(p, "nvrx_profiler_shutdown: null handle");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->initialized)
+        std::fprintf(stderr, "CuptiProfiler::shutdownProfiling called while not initialized.\n");
+    p->initialized = false;
+    p->started = false;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_start(nvrx_profiler* p) {
+    NVRX_CHECK_ARG(p, "nvrx_profiler_start: null handle");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->started) std::fprintf(stderr, "CuptiProfiler::startProfiling subsequent call.\n");
+    p->started = true;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_stop(nvrx_profiler* p) {
+    NVRX_CHECK_ARG(p, "nvrx_profiler_stop: null handle");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->started) std::fprintf(stderr, "CuptiProfiler::stopProfiling called while not profiling.\n");
+    p->started = false;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_reset(nvrx_profiler* p) {
+    NVRX_CHECK_ARG(p, "nvrx_profiler_reset: null handle");
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->staged.clear();  // CuptiProfiler.cpp:148-152: flush + clear all rings
+    p->log_n = 0;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_register_kernel(nvrx_profiler* p, const char* name, uint32_t* slot) {
+    NVRX_CHECK_ARG(p && name && slot, "nvrx_profiler_register_kernel: null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    auto it = p->name_to_slot.find(name);
+    if (it != p->name_to_slot.end()) {
+        *slot = it->second;
+        return NVRX_OK;
+    }
+    const uint32_t s = (uint32_t)p->names.size();
+    p->name_to_slot.emplace(name, s);
+    p->names.emplace_back(name);
+    *slot = s;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n) {
+    NVRX_CHECK_ARG(p && (n == 0 || recs) && n >= 0, "nvrx_profiler_push: bad arguments");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->started) return NVRX_OK;  // activity disabled: records are not captured
+    const uint32_t nslots = (uint32_t)p->names.size();
+    for (int64_t i = 0; i < n; ++i)
+        if (recs[i].slot >= nslots) return fail(NVRX_ERR_INVALID, "nvrx_profiler_push: unknown slot");
+    p->staged.insert(p->staged.end(), recs, recs + n);
+    return NVRX_OK;
+}
+
+int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
+                            int32_t* num, float* mn, float* mx, float* med, float* avg, float* sd) {
+    NVRX_CHECK_ARG(p && count, "nvrx_profiler_get_stats: null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    DeviceGuard g(p->cfg.device);
+    int rc = flush_locked(p);
+    if (rc) return rc;
+    *count = 0;
+    const int64_t nslots = (int64_t)p->names.size();
+    const size_t nb = (size_t)nslots * 4;
+    if (p->log_n == 0 || nslots == 0) return NVRX_OK;
+    if (nslots > nvrx_records_max_slots())
+        return fail(NVRX_ERR_INVALID, "nvrx_profiler_get_stats: too many distinct kernels");
+    Work w;
+    rc = bucket_log(p, nslots, 0, w);
+    if (rc) return rc;
+    nvrx_stats_soa soa{w.num, w.mn, w.mx, w.med, w.avg, w.sd};
+    const int64_t cap = p->cfg.stats_max_len_per_kernel;
+    hipError_t e = nvrx::segment_stats_ragged(w.ns, w.seg_off, w.seg_len, nslots,
+                                              std::min<int64_t>(cap, p->log_n), cap, p->cfg.mode,
+                                              true, soa, p->stream);
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: segment_stats");
+    std::vector<int32_t> hnum(nslots);
+    std::vector<float> hmn(nslots), hmx(nslots), hmed(nslots), havg(nslots), hsd(nslots);
+    struct {
+        void* dst;
+        const void* src;
+        size_t b;
+    } cps[] = {{hnum.data(), w.num, nb}, {hmn.data(), w.mn, nb},   {hmx.data(), w.mx, nb},
+               {hmed.data(), w.med, nb}, {havg.data(), w.avg, nb}, {hsd.data(), w.sd, nb}};
+    for (auto& c : cps) {
+        e = hipMemcpyAsync(c.dst, c.src, c.b, hipMemcpyDeviceToHost, p->stream);
+        if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: download");
+    }
+    e = hipStreamSynchronize(p->stream);
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: sync");
+    // std::map order of getStats (CuptiProfiler.cpp:137-145): sorted by composite name
+    std::vector<uint32_t> order;
+    for (int64_t s = 0; s < nslots; ++s)
+        if (hnum[s] > 0) order.push_back((uint32_t)s);
+    std::sort(order.begin(), order.end(),
+              [&](uint32_t a, uint32_t b) { return p->names[a] < p->names[b]; });
+    *count = (int64_t)order.size();
+    const int64_t m = std::min<int64_t>(cap_out, (int64_t)order.size());
+    for (int64_t i = 0; i < m; ++i) {
+        const uint32_t s = order[i];
+        if (slots) slots[i] = s;
+        if (num) num[i] = hnum[s];
+        if (mn) mn[i] = hmn[s];
+        if (mx) mx[i] = hmx[s];
+        if (med) med[i] = hmed[s];
+        if (avg) avg[i] = havg[s];
+        if (sd) sd[i] = hsd[s];
+    }
+    return NVRX_OK;
+}
+
+int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_t buflen) {
+    NVRX_CHECK_ARG(p && buf && buflen > 0, "nvrx_profiler_kernel_name: bad arguments");
+    std::lock_guard<std::mutex> lk(p->mu);
+    NVRX_CHECK_ARG(slot < p->names.size(), "nvrx_profiler_kernel_name: unknown slot");
+    const std::string& s = p->names[slot];
+    if ((int64_t)s.size() + 1 > buflen)
+        return fail(NVRX_ERR_INVALID, "nvrx_profiler_kernel_name: buffer too small");
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return NVRX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,91 @@
+// nvrx_common.h -- shared device helpers for the gfx950 straggler-scoring kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NVRX_WAVE 64
+
+namespace nvrx {
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Number of lanes below this one whose bit is set in mask.
+__device__ __forceinline__ unsigned mbcnt(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// ---- cross-lane reductions on DPP (pure VALU, no LDS crossbar, no index VGPRs) ----
+// Within each 16-lane row: quad_perm xor1 (0xB1), quad_perm xor2 (0x4E),
+// row_half_mirror (0x141), row_mirror (0x140) pair every lane with a distinct partner,
+// so after 4 steps every lane holds its row's result; the 4 row results are then
+// combined from lanes 0/16/32/48 in a fixed order (uniform, deterministic).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp(unsigned x) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const unsigned lo = dpp<CTRL>((unsigned)b), hi = dpp<CTRL>((unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ unsigned rl(unsigned x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ double rl(double x, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ unsigned wave_min_u32(unsigned v) {
+    v = min(v, dpp<0xB1>(v));
+    v = min(v, dpp<0x4E>(v));
+    v = min(v, dpp<0x141>(v));
+    v = min(v, dpp<0x140>(v));
+    return min(min(rl(v, 0), rl(v, 16)), min(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, dpp<0xB1>(v));
+    v = max(v, dpp<0x4E>(v));
+    v = max(v, dpp<0x141>(v));
+    v = max(v, dpp<0x140>(v));
+    return max(max(rl(v, 0), rl(v, 16)), max(rl(v, 32), rl(v, 48)));
+}
+__device__ __forceinline__ unsigned wave_sum_u32(unsigned v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
+}
+// Fixed pairing order: every lane ends with the same, run-to-run identical sum
+// (a + b == b + a exactly, so both partners of a pair agree).
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    v = v + dpp_f64<0xB1>(v);
+    v = v + dpp_f64<0x4E>(v);
+    v = v + dpp_f64<0x141>(v);
+    v = v + dpp_f64<0x140>(v);
+    return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
+}
+// Inclusive prefix sum over the 64 lanes: row_shr 1/2/4/8 (bound_ctrl zero-fills
+// lanes whose source is outside the row), then add the preceding rows' totals.
+__device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned v) {
+    v += dpp<0x111>(v);
+    v += dpp<0x112>(v);
+    v += dpp<0x114>(v);
+    v += dpp<0x118>(v);
+    const int l = lane_id();
+    const unsigned r0 = rl(v, 15), r1 = rl(v, 31), r2 = rl(v, 47);
+    v += (l >= 16 ? r0 : 0u) + (l >= 32 ? r1 : 0u) + (l >= 48 ? r2 : 0u);
+    return v;
+}
+
+// CuptiProfiler.cpp:187 -- (end - start) / 1000.0f: integer ns -> f32 (round to
+// nearest) -> correctly-rounded IEEE divide (hipcc lowers '/' to the
+// div_scale/div_fmas/div_fixup sequence; the build never enables fast-math).
+__device__ __forceinline__ float ns_to_us(unsigned ns) { return (float)ns / 1000.0f; }
+
+}  // namespace nvrx
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));

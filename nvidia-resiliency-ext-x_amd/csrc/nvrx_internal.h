@@ -1,0 +1,40 @@
+// nvrx_internal.h -- internal (C++) interfaces between the HIP kernel files and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/nvrx_straggler.h"
+
+namespace nvrx {
+
+hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
+                                 int64_t seg_begin, int64_t seg_len, int64_t cap, int mode,
+                                 const nvrx_stats_soa& out, hipStream_t st);
+hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
+                                int64_t nseg, int64_t max_len, int64_t cap, int mode,
+                                bool aligned16, const nvrx_stats_soa& out, hipStream_t st);
+
+hipError_t kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
+                      uint32_t* scratch, hipStream_t st);
+hipError_t pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
+                          const double* med_f64, const int32_t* ids_sec, int64_t nsec,
+                          float* times, int64_t total, hipStream_t st);
+hipError_t scores(const nvrx_score_args& a, hipStream_t st);
+hipError_t finalize_scores(const double* partials, int64_t R, int64_t nshards, int round_f32,
+                           double thr_rel, double thr_ind, double* gpu_rel, double* gpu_ind,
+                           uint8_t* strag_rel, uint8_t* strag_ind, int32_t* err, hipStream_t st);
+hipError_t section_scores(const double* med, const uint8_t* present, int64_t R, int64_t S,
+                          const float* ref_in, const int32_t* ref_index, float* ref_work,
+                          double* hist, int round_f32, double* out_rel, double* out_ind,
+                          int32_t* err, hipStream_t st);
+hipError_t stragglers(const double* score, int64_t n, double thr, uint8_t* mask, hipStream_t st);
+
+#define NVRX_RECORDS_MAX_LDS (144 * 1024)
+int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots);
+hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                          int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
+                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st);
+hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, const int64_t* dst_off,
+                            const uint32_t* ns, int64_t nslots, nvrx_record* out, hipStream_t st);
+
+}  // namespace nvrx

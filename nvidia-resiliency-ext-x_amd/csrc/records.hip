@@ -1,0 +1,171 @@
+// records.hip -- kernel-duration record streams -> per-kernel retained segments (gfx950).
+//
+// Replaces the per-record hot loop of CuptiProfiler::bufferCompleted
+// (straggler/cupti_src/CuptiProfiler.cpp:168-203: key lookup, then a push into that
+// key's CircularBuffer) and the ring itself (CircularBuffer.h:53-69: keeps the LAST
+// `capacity` pushes).  Records stay resident in HBM in push order; at report time each
+// stream (one per rank) is bucketed by slot and only the last `cap` records of every
+// slot are kept.  computeStats sorts, so order inside a bucket does not change any
+// statistic; buckets are still written in push order whenever a slot overflowed.
+//
+// One 64-lane wave owns one stream; per-slot counters live in LDS:
+//   pass 1: LDS histogram of slots;
+//   scan  : keep_s = min(count_s, cap), bucket starts padded to 16 B (aligned loads
+//           in segment_stats), written to seg_off / seg_len / counts;
+//   pass 2: scatter.  No slot overflowed -> LDS atomic slot cursors (order-free);
+//           else a stable pass: 64 records per step, same-slot lanes grouped with
+//           ballot (leader = lowest lane), occurrence index = cursor + mbcnt(group),
+//           record kept iff occurrence >= count - keep.
+#include "nvrx_common.h"
+#include "nvrx_internal.h"
+
+namespace nvrx {
+
+__device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t, int64_t nslots) {
+    return ((rec_off[t] + 3) & ~(int64_t)3) + t * (3 * nslots + 4);
+}
+
+__global__ __launch_bounds__(64) void records_bucket_kernel(const nvrx_record* __restrict__ recs,
+                                                            const int64_t* __restrict__ rec_off,
+                                                            int64_t nslots, int64_t cap,
+                                                            int force_stable, int64_t* seg_off,
+                                                            int32_t* seg_len, uint32_t* out_ns,
+                                                            int32_t* counts) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* cnt = lds;                // [nslots] pushes per slot
+    uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
+    uint32_t* start = lds + 2 * nslots; // [nslots] bucket start (relative to stream base)
+    const int64_t t = blockIdx.x;
+    const int lane = lane_id();
+    const int64_t r0 = rec_off[t], r1 = rec_off[t + 1];
+    const nvrx_record* rs = recs + r0;
+    const int64_t n = r1 - r0;
+    const int64_t base = stream_base(rec_off, t, nslots);
+
+    for (int64_t s = lane; s < nslots; s += 64) {
+        cnt[s] = 0u;
+        cur[s] = 0u;
+    }
+    __syncthreads();
+    for (int64_t i = lane; i < n; i += 64) {
+        const uint32_t s = rs[i].slot;
+        if (s < (uint32_t)nslots) atomicAdd(&cnt[s], 1u);
+    }
+    __syncthreads();
+
+    // exclusive scan of padded keeps over slots, 64 at a time with a running carry
+    uint32_t carry = 0;
+    bool overflow = false;
+    for (int64_t c = 0; c < nslots; c += 64) {
+        const int64_t s = c + lane;
+        uint32_t keep = 0, total = 0;
+        if (s < nslots) {
+            total = cnt[s];
+            keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+            overflow |= (keep != total);
+        }
+        const uint32_t padded = (keep + 3u) & ~3u;
+        const uint32_t incl = wave_incl_scan_u32(padded);
+        const uint32_t st = carry + incl - padded;
+        if (s < nslots) {
+            start[s] = st;
+            const int64_t g = t * nslots + s;
+            seg_off[g] = base + st;
+            seg_len[g] = (int32_t)keep;
+            counts[g] = (int32_t)total;
+        }
+        carry += __builtin_amdgcn_readlane(incl, 63);
+    }
+    overflow = (__ballot(overflow) != 0) || force_stable;
+    __syncthreads();
+    uint32_t* out = out_ns + base;
+
+    if (!overflow) {
+        for (int64_t i = lane; i < n; i += 64) {
+            const nvrx_record rec = rs[i];
+            if (rec.slot < (uint32_t)nslots) {
+                const uint32_t pos = atomicAdd(&cur[rec.slot], 1u);
+                out[start[rec.slot] + pos] = rec.ns;
+            }
+        }
+        return;
+    }
+    // stable pass: occurrence index of each record within its slot, push order
+    for (int64_t b = 0; b < n; b += 64) {
+        const int64_t i = b + lane;
+        const bool valid = i < n;
+        nvrx_record rec = {0xFFFFFFFFu, 0u};
+        if (valid) rec = rs[i];
+        const bool ok = valid && rec.slot < (uint32_t)nslots;
+        uint64_t pending = __ballot(ok);
+        uint32_t occ = 0;
+        while (pending) {
+            const int leader = __builtin_ffsll(pending) - 1;
+            const uint32_t ls = __builtin_amdgcn_readlane(rec.slot, leader);
+            const uint64_t grp = __ballot(ok && rec.slot == ls) & pending;
+            const uint32_t c0 = cur[ls];
+            if (rec.slot == ls && ok) occ = c0 + mbcnt(grp);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == leader) cur[ls] = c0 + (uint32_t)__popcll(grp);
+            __builtin_amdgcn_wave_barrier();
+            pending &= ~grp;
+        }
+        if (ok) {
+            const uint32_t total = cnt[rec.slot];
+            const uint32_t keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+            const uint32_t drop = total - keep;
+            if (occ >= drop) out[start[rec.slot] + (occ - drop)] = rec.ns;
+        }
+    }
+}
+
+int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
+    return ((n + 3) & ~(int64_t)3) + nstreams * (3 * nslots + 4);
+}
+
+hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                          int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
+                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st) {
+    if (nstreams <= 0 || nslots <= 0) return hipSuccess;
+    const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
+    if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set && lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           NVRX_RECORDS_MAX_LDS);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(records_bucket_kernel, dim3((unsigned)nstreams), dim3(64), lds, st, recs,
+                       rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts);
+    return hipGetLastError();
+}
+
+// Turn retained buckets back into a record stream (slot-major, push order kept inside a
+// slot): used to compact a long-lived device record log without changing which records
+// a later retention step keeps.  dst_off[s] = first output index of slot s.
+__global__ void records_unbucket_kernel(const int64_t* seg_off, const int32_t* seg_len,
+                                        const int64_t* dst_off, const uint32_t* ns, int64_t nslots,
+                                        nvrx_record* out) {
+    const int64_t s = blockIdx.x;
+    if (s >= nslots) return;
+    const int64_t b = seg_off[s], d = dst_off[s];
+    const int32_t len = seg_len[s];
+    for (int32_t i = threadIdx.x; i < len; i += blockDim.x) {
+        nvrx_record r;
+        r.slot = (uint32_t)s;
+        r.ns = ns[b + i];
+        out[d + i] = r;
+    }
+}
+
+hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, const int64_t* dst_off,
+                            const uint32_t* ns, int64_t nslots, nvrx_record* out, hipStream_t st) {
+    if (nslots <= 0) return hipSuccess;
+    hipLaunchKernelGGL(records_unbucket_kernel, dim3((unsigned)nslots), dim3(256), 0, st, seg_off,
+                       seg_len, dst_off, ns, nslots, out);
+    return hipGetLastError();
+}
+
+}  // namespace nvrx

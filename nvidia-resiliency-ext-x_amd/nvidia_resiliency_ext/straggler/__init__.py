@@ -1,0 +1,6 @@
+"""Straggler detection, MI355X-native (drop-in for nvidia_resiliency_ext.straggler).
+
+Exports the reference's public names (reference straggler/__init__.py:16-18) plus
+``StragglerReport`` (alias of ``Report``).
+"""
+from .statistics import Statistic  # noqa: F401

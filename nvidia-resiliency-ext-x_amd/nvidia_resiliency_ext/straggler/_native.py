@@ -1,0 +1,159 @@
+"""ctypes binding of libnvrx_hip.so, the C ABI declared in include/nvrx_straggler.h.
+
+The shared library holds the hand-written gfx950 kernels of the scoring path.  There is
+no CPU fallback: if the library is missing or fails to load, every entry point raises.
+Device arrays are passed as raw pointers (torch tensors' ``data_ptr()``), streams as the
+HIP stream handle (``torch.cuda.current_stream().cuda_stream``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+LIB_NAME = "libnvrx_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+NVRX_OK = 0
+NVRX_ERR_INVALID = -1
+NVRX_ERR_HIP = -2
+NVRX_ERR_STATE = -3
+NVRX_ERR_SINGLETON = -4
+NVRX_ERR_NOMEM = -5
+
+NVRX_STATS_FAST = 0
+NVRX_STATS_EXACT = 1
+NVRX_MAX_SEGMENT = 32768
+
+P = ctypes.c_void_p
+i32 = ctypes.c_int32
+i64 = ctypes.c_int64
+u32 = ctypes.c_uint32
+f64 = ctypes.c_double
+
+
+class StatsSoA(ctypes.Structure):
+    _fields_ = [("num", P), ("min", P), ("max", P), ("med", P), ("avg", P), ("std", P)]
+
+
+class ScoreArgs(ctypes.Structure):
+    _fields_ = [
+        ("R", i64), ("K", i64),
+        ("num", P), ("med", P), ("avg", P), ("col_valid", P),
+        ("ref", P), ("ref_index", P),
+        ("hist", P), ("hist_index", P), ("hist_stride", i64),
+        ("partials", P), ("err", P),
+    ]
+
+
+class Record(ctypes.Structure):
+    _fields_ = [("slot", u32), ("ns", u32)]
+
+
+class ProfilerConfig(ctypes.Structure):
+    _fields_ = [
+        ("buffer_size", i64), ("num_buffers", i64), ("stats_max_len_per_kernel", i64),
+        ("device", i32), ("mode", i32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol the header declares
+SIGNATURES = {
+    "nvrx_last_error": (ctypes.c_char_p, []),
+    "nvrx_abi_version": (ctypes.c_int, []),
+    "nvrx_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "nvrx_sync": (ctypes.c_int, [P]),
+    "nvrx_segment_stats_strided": (ctypes.c_int, [P, i64, i64, i64, i64, i64, i32,
+                                                  ctypes.POINTER(StatsSoA), P]),
+    "nvrx_segment_stats_ragged": (ctypes.c_int, [P, P, P, i64, i64, i64, i32, i32,
+                                                 ctypes.POINTER(StatsSoA), P]),
+    "nvrx_kernel_ref": (ctypes.c_int, [P, P, i64, i64, P, P, P]),
+    "nvrx_pack_min_times": (ctypes.c_int, [P, P, i64, P, P, i64, P, i64, P]),
+    "nvrx_scores": (ctypes.c_int, [ctypes.POINTER(ScoreArgs), P]),
+    "nvrx_finalize_scores": (ctypes.c_int, [P, i64, i64, i32, f64, f64, P, P, P, P, P, P]),
+    "nvrx_section_scores": (ctypes.c_int, [P, P, i64, i64, P, P, P, P, i32, P, P, P, P]),
+    "nvrx_stragglers": (ctypes.c_int, [P, i64, f64, P, P]),
+    "nvrx_records_bucket_capacity": (i64, [i64, i64, i64]),
+    "nvrx_records_bucket": (ctypes.c_int, [P, P, i64, i64, i64, P, P, P, P, P]),
+    "nvrx_records_max_slots": (i64, []),
+    "nvrx_profiler_create": (ctypes.c_int, [ctypes.POINTER(ProfilerConfig), ctypes.POINTER(P)]),
+    "nvrx_profiler_destroy": (ctypes.c_int, [P]),
+    "nvrx_profiler_initialize": (ctypes.c_int, [P]),
+    "nvrx_profiler_shutdown": (ctypes.c_int, [P]),
+    "nvrx_profiler_start": (ctypes.c_int, [P]),
+    "nvrx_profiler_stop": (ctypes.c_int, [P]),
+    "nvrx_profiler_reset": (ctypes.c_int, [P]),
+    "nvrx_profiler_register_kernel": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.POINTER(u32)]),
+    "nvrx_profiler_push": (ctypes.c_int, [P, P, i64]),
+    "nvrx_profiler_get_stats": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P, P, P, P, P, P, P]),
+    "nvrx_profiler_kernel_name": (ctypes.c_int, [P, u32, ctypes.c_char_p, i64]),
+    "nvrx_profiler_capture_available": (ctypes.c_int, []),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libnvrx_hip.so (once).  Raises NativeLibraryError if it is missing: the HIP
+    path is the product; nothing falls back to the CPU."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                f"{LIB_NAME} not found at {LIB_PATH}; build it with "
+                f"`make -C nvidia-resiliency-ext-x_amd/csrc` (hipcc --offload-arch=gfx950)")
+        try:
+            L = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.nvrx_abi_version() != 1:
+            raise NativeLibraryError("libnvrx_hip.so ABI version mismatch")
+        _lib = L
+        return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    """Map a status code to the reference's error behaviour (RuntimeError)."""
+    if rc != NVRX_OK:
+        msg = lib().nvrx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg}" if what else msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def ptr(t) -> Optional[int]:
+    """Device (or host) pointer of a tensor / numpy array; None passes NULL."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_handle(stream=None) -> Optional[int]:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def require_device(t, name: str = "tensor") -> None:
+    """Kernels only ever see device memory: a CPU tensor is a caller bug, raised loudly."""
+    if t is not None and (not hasattr(t, "is_cuda") or not t.is_cuda):
+        raise ValueError(f"{name} must be a device (HIP) tensor")

@@ -1,0 +1,181 @@
+"""Torch-tensor front end of the HIP kernels (thin: allocation + argument marshalling).
+
+Every function takes/returns device tensors and enqueues work on the current HIP stream;
+all arithmetic happens in libnvrx_hip.so.  Shape checks run on the host before any
+launch (the C layer re-checks).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from . import _native as N
+
+STATS_FAST = N.NVRX_STATS_FAST
+STATS_EXACT = N.NVRX_STATS_EXACT
+
+
+@dataclass
+class SegmentStats:
+    """SoA statistics of a batch of segments (device tensors, float32 microseconds)."""
+
+    num: torch.Tensor
+    min: torch.Tensor
+    max: torch.Tensor
+    med: torch.Tensor
+    avg: torch.Tensor
+    std: torch.Tensor
+
+    @classmethod
+    def empty(cls, n: int, device) -> "SegmentStats":
+        f = lambda dt: torch.empty(n, dtype=dt, device=device)  # noqa: E731
+        return cls(f(torch.int32), f(torch.float32), f(torch.float32), f(torch.float32),
+                   f(torch.float32), f(torch.float32))
+
+    def view(self, *shape) -> "SegmentStats":
+        return SegmentStats(*(getattr(self, k).view(*shape) for k in
+                              ("num", "min", "max", "med", "avg", "std")))
+
+    def soa(self) -> N.StatsSoA:
+        return N.StatsSoA(self.num.data_ptr(), self.min.data_ptr(), self.max.data_ptr(),
+                          self.med.data_ptr(), self.avg.data_ptr(), self.std.data_ptr())
+
+    def cpu(self) -> "SegmentStats":
+        return SegmentStats(*(getattr(self, k).cpu() for k in
+                              ("num", "min", "max", "med", "avg", "std")))
+
+
+def _stream(stream):
+    return N.stream_handle(stream)
+
+
+def segment_stats_strided(ns: torch.Tensor, nseg: int, seg_stride: int, seg_begin: int,
+                          seg_len: int, cap: int = 0, mode: int = STATS_FAST,
+                          out: Optional[SegmentStats] = None, stream=None) -> SegmentStats:
+    """Stats of segments ns.flat[s*seg_stride + seg_begin : +seg_len] (uint32 ns), last
+    `cap` samples retained (CircularBuffer.h:53-69).  reference: CuptiProfiler.cpp:44-74."""
+    N.require_device(ns, "ns")
+    if ns.dtype not in (torch.int32, torch.uint32):
+        raise TypeError("ns must be a 32-bit integer tensor of nanosecond durations")
+    if nseg > 0 and (nseg - 1) * seg_stride + seg_begin + seg_len > ns.numel():
+        raise ValueError("segments exceed the ns tensor")
+    if out is None:
+        out = SegmentStats.empty(nseg, ns.device)
+    soa = out.soa()
+    N.call("nvrx_segment_stats_strided", ns.data_ptr(), nseg, seg_stride, seg_begin, seg_len,
+           cap, mode, ctypes.byref(soa), _stream(stream))
+    return out
+
+
+def segment_stats_ragged(ns: torch.Tensor, seg_off: torch.Tensor, seg_len: Optional[torch.Tensor],
+                         max_len: int, cap: int = 0, mode: int = STATS_FAST, aligned16: bool = False,
+                         out: Optional[SegmentStats] = None, stream=None) -> SegmentStats:
+    N.require_device(ns, "ns")
+    N.require_device(seg_off, "seg_off")
+    nseg = seg_off.numel() - (0 if seg_len is not None else 1)
+    if seg_off.dtype != torch.int64 or (seg_len is not None and seg_len.dtype != torch.int32):
+        raise TypeError("seg_off must be int64 and seg_len int32")
+    if out is None:
+        out = SegmentStats.empty(max(nseg, 0), ns.device)
+    soa = out.soa()
+    N.call("nvrx_segment_stats_ragged", ns.data_ptr(), seg_off.data_ptr(),
+           N.ptr(seg_len), nseg, max_len, cap, mode, int(aligned16), ctypes.byref(soa),
+           _stream(stream))
+    return out
+
+
+def kernel_ref(num: torch.Tensor, med: torch.Tensor, ref: Optional[torch.Tensor] = None,
+               scratch: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """ref[k] = min_r med[r, k] if every row has k (num > 0), else NaN (reporting.py:255-296)."""
+    R, K = med.shape
+    if ref is None:
+        ref = torch.empty(K, dtype=torch.float32, device=med.device)
+    if scratch is None:
+        scratch = torch.empty(2 * K, dtype=torch.int32, device=med.device)
+    N.call("nvrx_kernel_ref", num.data_ptr(), med.data_ptr(), R, K, ref.data_ptr(),
+           scratch.data_ptr(), _stream(stream))
+    return ref
+
+
+def pack_min_times(med_f32: torch.Tensor, ids: torch.Tensor, med_f64: torch.Tensor,
+                   ids_sec: torch.Tensor, total: int, out: Optional[torch.Tensor] = None,
+                   stream=None) -> torch.Tensor:
+    dev = med_f32.device
+    if out is None:
+        out = torch.empty(total, dtype=torch.float32, device=dev)
+    N.call("nvrx_pack_min_times", med_f32.data_ptr(), ids.data_ptr(), med_f32.numel(),
+           med_f64.data_ptr(), ids_sec.data_ptr(), med_f64.numel(), out.data_ptr(), total,
+           _stream(stream))
+    return out
+
+
+def scores(num, med, avg, *, col_valid=None, ref=None, ref_index=None, hist=None,
+           hist_index=None, hist_stride=0, partials=None, err=None, stream=None) -> torch.Tensor:
+    """Per-row partial sums {sum s*w, sum w, n} for rel and indiv (reporting.py:219-253)."""
+    R, K = med.shape
+    if partials is None:
+        partials = torch.empty((R, 6), dtype=torch.float64, device=med.device)
+    a = N.ScoreArgs(R, K, num.data_ptr(), med.data_ptr(), avg.data_ptr(), N.ptr(col_valid),
+                    N.ptr(ref), N.ptr(ref_index), N.ptr(hist), N.ptr(hist_index), hist_stride,
+                    partials.data_ptr(), N.ptr(err))
+    N.call("nvrx_scores", ctypes.byref(a), _stream(stream))
+    return partials
+
+
+def finalize_scores(partials: torch.Tensor, R: int, nshards: int = 1, round_f32: bool = False,
+                    thr_rel: float = 0.75, thr_ind: float = 0.75, rel=True, ind=True, err=None,
+                    stream=None):
+    dev = partials.device
+    gr = torch.empty(R, dtype=torch.float64, device=dev) if rel else None
+    gi = torch.empty(R, dtype=torch.float64, device=dev) if ind else None
+    sr = torch.empty(R, dtype=torch.uint8, device=dev) if rel else None
+    si = torch.empty(R, dtype=torch.uint8, device=dev) if ind else None
+    N.call("nvrx_finalize_scores", partials.data_ptr(), R, nshards, int(round_f32),
+           float(thr_rel), float(thr_ind), N.ptr(gr), N.ptr(gi), N.ptr(sr), N.ptr(si),
+           N.ptr(err), _stream(stream))
+    return gr, gi, sr, si
+
+
+def section_scores(med: torch.Tensor, present: torch.Tensor, *, ref_in=None, ref_index=None,
+                   hist=None, round_f32=False, rel=True, ind=True, err=None, stream=None):
+    R, S = med.shape
+    dev = med.device
+    out_rel = torch.empty((R, S), dtype=torch.float64, device=dev) if rel else None
+    out_ind = torch.empty((R, S), dtype=torch.float64, device=dev) if ind else None
+    ref_work = torch.empty(S, dtype=torch.float32, device=dev) if (rel and ref_in is None) else None
+    N.call("nvrx_section_scores", med.data_ptr(), present.data_ptr(), R, S, N.ptr(ref_in),
+           N.ptr(ref_index), N.ptr(ref_work), N.ptr(hist), int(round_f32), N.ptr(out_rel),
+           N.ptr(out_ind), N.ptr(err), _stream(stream))
+    return out_rel, out_ind
+
+
+def stragglers(score: torch.Tensor, thr: float, out: Optional[torch.Tensor] = None, stream=None):
+    if out is None:
+        out = torch.empty(score.numel(), dtype=torch.uint8, device=score.device)
+    N.call("nvrx_stragglers", score.data_ptr(), score.numel(), float(thr), out.data_ptr(),
+           _stream(stream))
+    return out
+
+
+def records_bucket_capacity(n: int, nstreams: int, nslots: int) -> int:
+    return int(N.lib().nvrx_records_bucket_capacity(n, nstreams, nslots))
+
+
+def records_bucket(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: int, stream=None):
+    """recs: [n, 2] uint32/int32 {slot, ns}; rec_off: [nstreams+1] int64 (device).
+    Returns (seg_off int64 [nstreams*nslots], seg_len int32, out_ns, counts int32)."""
+    nstreams = rec_off.numel() - 1
+    dev = recs.device
+    n = recs.shape[0]
+    cap_ns = records_bucket_capacity(n, nstreams, nslots)
+    seg_off = torch.empty(nstreams * nslots, dtype=torch.int64, device=dev)
+    seg_len = torch.empty(nstreams * nslots, dtype=torch.int32, device=dev)
+    counts = torch.empty(nstreams * nslots, dtype=torch.int32, device=dev)
+    out_ns = torch.empty(max(cap_ns, 1), dtype=torch.int32, device=dev)
+    N.call("nvrx_records_bucket", recs.data_ptr(), rec_off.data_ptr(), nstreams, nslots, cap,
+           seg_off.data_ptr(), seg_len.data_ptr(), out_ns.data_ptr(), counts.data_ptr(),
+           _stream(stream))
+    return seg_off, seg_len, out_ns, counts

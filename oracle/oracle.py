@@ -1,0 +1,176 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front end of the C oracle (oracle/nvrx_oracle.c).
+
+The oracle is the parity checker for the HIP product path and the timed host-CPU
+Reporter of bench.py (cpu_baseline.kind = "port").  Only tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg may import this module; the product package never does.
+
+Pinning: tests/test_oracle_golden.py checks every function here against
+tests/golden/*.json, which tests/golden/make_golden.py produced from the reference
+itself (computeStats compiled from /root/reference by oracle/Makefile; the
+reference ReportGenerator run on gloo).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+SEED = 0x5EED
+SEED2 = 0xBA5E
+
+
+class KStats(ctypes.Structure):
+    _fields_ = [
+        ("num_calls", ctypes.c_int32),
+        ("min", ctypes.c_float),
+        ("max", ctypes.c_float),
+        ("median", ctypes.c_float),
+        ("avg", ctypes.c_float),
+        ("stddev", ctypes.c_float),
+    ]
+
+
+def build() -> str:
+    """Compile liboracle.so (gcc) if missing or stale."""
+    src = os.path.join(_HERE, "nvrx_oracle.c")
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "all"])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        i64 = ctypes.c_int64
+        u64 = ctypes.c_uint64
+        L.oracle_splitmix64.restype = u64
+        L.oracle_splitmix64.argtypes = [u64]
+        L.oracle_base_ns.restype = u64
+        L.oracle_base_ns.argtypes = [u64, u64]
+        L.oracle_sample_ns.restype = ctypes.c_uint32
+        L.oracle_sample_ns.argtypes = [u64, u64, u64, u64, u64, u64, u64, ctypes.c_int]
+        L.oracle_gen_matrix.argtypes = [P, i64, i64, i64, u64, u64, P]
+        L.oracle_ns_to_us.restype = ctypes.c_float
+        L.oracle_ns_to_us.argtypes = [u64]
+        L.oracle_compute_stats.argtypes = [P, i64, ctypes.POINTER(KStats)]
+        L.oracle_ring_linearize.restype = i64
+        L.oracle_ring_linearize.argtypes = [P, i64, i64, P]
+        L.oracle_matrix_stats.argtypes = [P, i64, i64, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
+        L.oracle_kernel_ref.argtypes = [P, P, i64, i64, P]
+        L.oracle_scores.argtypes = [P, P, P, i64, i64, P, P, P, P, P]
+        L.oracle_stragglers.restype = i64
+        L.oracle_stragglers.argtypes = [P, i64, ctypes.c_double, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+# ---------------------------------------------------------------- generator
+def splitmix64(x: int) -> int:
+    return int(lib().oracle_splitmix64(x & 0xFFFFFFFFFFFFFFFF))
+
+
+def straggler_ranks(R: int, seed: int = SEED, frac_div: int = 100) -> np.ndarray:
+    """Seeded straggler-rank flags: max(1, R // frac_div) draws of splitmix64 % R."""
+    flags = np.zeros(R, dtype=np.uint8)
+    n = max(1, R // frac_div)
+    for j in range(n):
+        flags[splitmix64(seed ^ (0xC0FFEE + j)) % R] = 1
+    return flags
+
+
+def gen_matrix(R, K, s_push, seed=SEED, seed2=SEED2, straggler=None) -> np.ndarray:
+    if straggler is None:
+        straggler = straggler_ranks(R, seed)
+    straggler = np.ascontiguousarray(straggler, dtype=np.uint8)
+    out = np.empty((R, K, s_push), dtype=np.uint32)
+    lib().oracle_gen_matrix(_p(out), R, K, s_push, seed, seed2, _p(straggler))
+    return out
+
+
+# ---------------------------------------------------------------- statistics
+def ns_to_us(ns) -> np.ndarray:
+    """CuptiProfiler.cpp:187 conversion, elementwise (u64 -> f32 RN, then / 1000.0f)."""
+    ns = np.asarray(ns, dtype=np.uint64)
+    f = ns.astype(np.float32)  # RN, exact below 2**24
+    return (f / np.float32(1000.0)).astype(np.float32)
+
+
+def compute_stats(values_f32) -> KStats:
+    v = np.ascontiguousarray(values_f32, dtype=np.float32)
+    st = KStats()
+    lib().oracle_compute_stats(_p(v), v.size, ctypes.byref(st))
+    return st
+
+
+def ring_linearize(pushed_f32, cap: int) -> np.ndarray:
+    v = np.ascontiguousarray(pushed_f32, dtype=np.float32)
+    out = np.empty(min(v.size, cap), dtype=np.float32)
+    n = lib().oracle_ring_linearize(_p(v), v.size, cap, _p(out))
+    return out[:n]
+
+
+def matrix_stats(ns: np.ndarray, nseg: int, seg_stride: int, seg_begin: int, seg_len: int,
+                 cap: int = 0, nthreads: int = 1) -> dict:
+    """Stats of segments ns.flat[s*seg_stride+seg_begin : +seg_len], last `cap` kept."""
+    ns = np.ascontiguousarray(ns, dtype=np.uint32)
+    out = {
+        "num": np.empty(nseg, np.int32),
+        "min": np.empty(nseg, np.float32),
+        "max": np.empty(nseg, np.float32),
+        "med": np.empty(nseg, np.float32),
+        "avg": np.empty(nseg, np.float32),
+        "std": np.empty(nseg, np.float32),
+    }
+    lib().oracle_matrix_stats(_p(ns), nseg, seg_stride, seg_begin, seg_len, cap,
+                              _p(out["num"]), _p(out["min"]), _p(out["max"]), _p(out["med"]),
+                              _p(out["avg"]), _p(out["std"]), int(nthreads))
+    return out
+
+
+# ---------------------------------------------------------------- scoring
+def kernel_ref(num: np.ndarray, med: np.ndarray) -> np.ndarray:
+    R, K = num.shape
+    ref = np.empty(K, np.float32)
+    lib().oracle_kernel_ref(_p(np.ascontiguousarray(num, np.int32)),
+                            _p(np.ascontiguousarray(med, np.float32)), R, K, _p(ref))
+    return ref
+
+
+def scores(num, med, avg, col_valid=None, ref=None, hist=None, rel=True, indiv=True):
+    """Returns (gpu_rel[R] or None, gpu_ind[R] or None); hist ([R][K] f64) is updated."""
+    num = np.ascontiguousarray(num, np.int32)
+    med = np.ascontiguousarray(med, np.float32)
+    avg = np.ascontiguousarray(avg, np.float32)
+    R, K = num.shape
+    if ref is None:
+        ref = kernel_ref(num, med)
+    ref = np.ascontiguousarray(ref, np.float32)
+    if col_valid is not None:
+        col_valid = np.ascontiguousarray(col_valid, np.uint8)
+    if hist is None:
+        hist = np.full((R, K), np.inf, np.float64)
+    gr = np.empty(R, np.float64) if rel else None
+    gi = np.empty(R, np.float64) if indiv else None
+    lib().oracle_scores(_p(num), _p(med), _p(avg), R, K, _p(col_valid), _p(ref), _p(hist),
+                        _p(gr), _p(gi))
+    return gr, gi
+
+
+def stragglers(score: np.ndarray, thr: float) -> np.ndarray:
+    score = np.ascontiguousarray(score, np.float64)
+    mask = np.empty(score.size, np.uint8)
+    lib().oracle_stragglers(_p(score), score.size, float(thr), _p(mask))
+    return mask

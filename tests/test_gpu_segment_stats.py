@@ -1,0 +1,187 @@
+"""GPU parity: per-kernel statistics (HIP segment_stats) vs the oracle computeStats.
+
+Bar (north_star): NUM / MIN / MAX / MED bit-exact on integer-ns inputs, in both modes;
+EXACT mode also AVG / STD bit-exact; FAST mode AVG / STD are the exact f64 mean /
+population std of the retained samples rounded once to f32, checked (a) against an f64
+numpy reference within 2 f32 ulps and (b) against the oracle's sequential-f32 values
+within rtol 1e-4 (the reference's own accumulation error at n <= 8192).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from nvidia_resiliency_ext.straggler import ops, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+FIELDS = ("num", "min", "max", "med")
+
+
+def _oracle_segments(host_ns, nseg, stride, begin, length, cap):
+    return O.matrix_stats(host_ns, nseg, stride, begin, length, cap, nthreads=8)
+
+
+def _exact_avg_std(host_ns, nseg, stride, begin, length, cap):
+    keep = min(length, cap) if cap > 0 else length
+    avg = np.empty(nseg)
+    std = np.empty(nseg)
+    for s in range(nseg):
+        seg = host_ns[s * stride + begin + length - keep: s * stride + begin + length].astype(np.float64)
+        avg[s] = seg.mean() / 1000.0
+        std[s] = seg.std() / 1000.0
+    return avg, std
+
+
+def _check(gpu, ref, exact_fields=FIELDS, avg_std=None):
+    g = gpu.cpu()
+    for f in exact_fields:
+        a = getattr(g, f).numpy()
+        b = ref[f]
+        if a.dtype.kind == "f":
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (f, a[:8], b[:8])
+        else:
+            assert np.array_equal(a, b), (f, a[:8], b[:8])
+    if avg_std is not None:
+        # FAST: exact mean/std rounded once to f32.  A segment that does not fit a fast
+        # wave (>8192 slots incl. 16-B misalignment) runs the EXACT kernel instead, whose
+        # AVG/STD are the reference's own (bit-exact with the oracle): accept either.
+        avg, std = avg_std
+        ga, gs = g.avg.numpy(), g.std.numpy()
+        exact_ref = (ga.view(np.uint32) == ref["avg"].view(np.uint32)) & \
+                    (gs.view(np.uint32) == ref["std"].view(np.uint32))
+        fast_ok = (np.abs(ga - avg) <= 2.5e-7 * np.abs(avg)) & \
+                  (np.abs(gs - std) <= 1e-6 * np.abs(std) + 1e-6)
+        assert np.all(exact_ref | fast_ok), (ga, avg, ref["avg"])
+        np.testing.assert_allclose(ga, ref["avg"], rtol=1e-4)
+
+
+def test_synth_matrix_matches_oracle_generator():
+    R, K, S = 3, 7, 37
+    strag = synth.straggler_ranks(R)
+    g = synth.synth_matrix(R, K, S, device=DEV).cpu().numpy().view(np.uint32)
+    h = O.gen_matrix(R, K, S, straggler=strag)
+    assert np.array_equal(g, h)
+    # sharded columns: local column kk holds global kernel kmap[kk]
+    kmap = np.array([5, 1, 6], dtype=np.int64)
+    g2 = synth.synth_matrix(R, 3, S, K_global=K, kmap=torch.from_numpy(kmap).to(DEV),
+                            device=DEV).cpu().numpy().view(np.uint32)
+    assert np.array_equal(g2, h[:, kmap, :])
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_FAST, ops.STATS_EXACT])
+def test_matrix_config_small(mode):
+    # config-2 shape scaled down: S_push 10000 pushed, last 8192 retained
+    R, K, S = 2, 12, 10000
+    ns = synth.synth_matrix(R, K, S, device=DEV)
+    st = ops.segment_stats_strided(ns.view(-1), R * K, S, 0, S, cap=8192, mode=mode)
+    host = ns.cpu().numpy().view(np.uint32).reshape(-1)
+    ref = _oracle_segments(host, R * K, S, 0, S, 8192)
+    if mode == ops.STATS_EXACT:
+        _check(st, ref, exact_fields=FIELDS + ("avg", "std"))
+    else:
+        _check(st, ref, avg_std=_exact_avg_std(host, R * K, S, 0, S, 8192))
+
+
+LENGTHS = [1, 2, 3, 4, 5, 7, 8, 63, 64, 65, 255, 256, 257, 511, 512, 1000, 1023, 1024, 1025,
+           2047, 2048, 2049, 4095, 4096, 4097, 8191, 8192]
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_FAST, ops.STATS_EXACT])
+@pytest.mark.parametrize("length", LENGTHS)
+def test_lengths_and_alignment(mode, length):
+    rng = np.random.default_rng(length)
+    nseg = 6
+    for begin in (0, 1, 2, 3):
+        stride = length + begin + (rng.integers(0, 5) if begin else 0)
+        host = rng.integers(1000, 3_000_000, size=nseg * stride, dtype=np.uint32)
+        ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+        st = ops.segment_stats_strided(ns, nseg, stride, begin, length, cap=0, mode=mode)
+        ref = _oracle_segments(host, nseg, stride, begin, length, 0)
+        if mode == ops.STATS_EXACT:
+            _check(st, ref, exact_fields=FIELDS + ("avg", "std"))
+        else:
+            _check(st, ref, avg_std=_exact_avg_std(host, nseg, stride, begin, length, 0))
+
+
+def _edge_segments(n):
+    rng = np.random.default_rng(7)
+    segs = [
+        np.full(n, 12345, np.uint32),                                   # all equal
+        np.where(rng.random(n) < 0.5, 10, 20).astype(np.uint32),       # two values
+        rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32),  # full 32-bit range
+        (2**24 + rng.integers(-3, 4, size=n)).astype(np.uint32),       # u32->f32 rounding edge
+        np.sort(rng.integers(100, 200, size=n).astype(np.uint32)),     # sorted, narrow
+        np.sort(rng.integers(100, 2**31, size=n).astype(np.uint32))[::-1].copy(),  # reverse
+        # one huge bucket: most values clustered, few outliers (forces deeper levels)
+        np.concatenate([np.full(n - min(n, 3), 1_000_000, np.uint32) +
+                        rng.integers(0, 7, size=n - min(n, 3)).astype(np.uint32),
+                        np.array([1, 4_000_000_000, 7][:min(n, 3)], np.uint32)]),
+        (rng.integers(0, 2**20, size=n) * 4096 + 5).astype(np.uint32),  # sparse keys
+        np.zeros(n, np.uint32),                                          # 0-ns durations
+    ]
+    return segs
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_FAST, ops.STATS_EXACT])
+@pytest.mark.parametrize("n", [1, 2, 5, 64, 100, 1024, 3000, 8192])
+def test_edge_distributions(mode, n):
+    segs = _edge_segments(n)
+    host = np.concatenate(segs)
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    st = ops.segment_stats_strided(ns, len(segs), n, 0, n, cap=0, mode=mode)
+    ref = _oracle_segments(host, len(segs), n, 0, n, 0)
+    if mode == ops.STATS_EXACT:
+        _check(st, ref, exact_fields=FIELDS + ("avg", "std"))
+    else:
+        _check(st, ref)
+        avg, std = _exact_avg_std(host, len(segs), n, 0, n, 0)
+        g = st.cpu()
+        np.testing.assert_allclose(g.avg.numpy(), avg, rtol=2.5e-7, atol=1e-30)
+        np.testing.assert_allclose(g.std.numpy(), std, rtol=1e-6, atol=1e-6 * avg.max())
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_FAST, ops.STATS_EXACT])
+def test_ragged_segments(mode):
+    rng = np.random.default_rng(11)
+    lens = np.array([0, 1, 3, 17, 64, 257, 1000, 4096, 8192, 9000, 20000, 5, 2], np.int64)
+    cap = 8192
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    host = rng.integers(2000, 2_200_000, size=int(off[-1]), dtype=np.uint32)
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    st = ops.segment_stats_ragged(ns, torch.from_numpy(off).to(DEV), None,
+                                  max_len=int(lens.max()), cap=cap, mode=mode)
+    g = st.cpu()
+    for s, L in enumerate(lens):
+        seg = host[off[s]:off[s + 1]]
+        if L == 0:
+            assert g.num[s].item() == 0 and np.isnan(g.med[s].item())
+            continue
+        r = O.compute_stats(O.ns_to_us(seg[-min(L, cap):]))
+        assert g.num[s].item() == r.num_calls
+        for f, rf in (("min", "min"), ("max", "max"), ("med", "median")):
+            assert np.float32(getattr(g, f)[s].item()) == np.float32(getattr(r, rf)), (s, f)
+        if mode == ops.STATS_EXACT:
+            assert np.float32(g.avg[s].item()) == np.float32(r.avg)
+            assert np.float32(g.std[s].item()) == np.float32(r.stddev)
+        else:
+            assert abs(g.avg[s].item() - r.avg) <= 1e-4 * r.avg
+
+
+def test_ring_cap_seven():
+    # test_cupti_ext.py:107-127: statsMaxLenPerKernel=7, 21 pushes -> num_calls == 7
+    host = np.arange(1, 22, dtype=np.uint32) * 1000
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    for mode in (ops.STATS_FAST, ops.STATS_EXACT):
+        g = ops.segment_stats_strided(ns, 1, 21, 0, 21, cap=7, mode=mode).cpu()
+        assert g.num[0].item() == 7
+        assert g.min[0].item() == 15.0 and g.max[0].item() == 21.0 and g.med[0].item() == 18.0
+
+
+def test_shape_errors_raise():
+    ns = torch.zeros(100, dtype=torch.int32, device=DEV)
+    with pytest.raises(ValueError):
+        ops.segment_stats_strided(ns, 2, 60, 0, 60)
+    with pytest.raises(RuntimeError):
+        ops.segment_stats_strided(ns, 1, 100, 0, 100, cap=0, mode=7)
