@@ -24,6 +24,7 @@
  *                          float32 rounding of _get_tensor_from_scores                    reporting.py:251-253, 338-361
  *   nvrx_section_scores    _compute_sections_perf_scores (+ section MIN reduce, history)  reporting.py:196-217, 255-314
  *   nvrx_stragglers        Report.identify_stragglers (score < threshold, strict)         reporting.py:84-151
+ *   nvrx_section_stats     Detector._get_section_summaries (torch f64 stats)             straggler.py:171-197
  *   nvrx_profiler_*        nvrx_cupti_module.CuptiProfiler (ctor, initialize, shutdown,
  *                          start, stop, get_stats, reset)                                 cupti_src/cupti_module_py.cpp:33-54
  *   nvrx_records_*         CuptiProfiler::bufferCompleted record loop + CircularBuffer     cupti_src/CuptiProfiler.cpp:168-203, CircularBuffer.h:53-69
@@ -64,19 +65,23 @@ typedef struct nvrx_stats_soa {
     float* std;
 } nvrx_stats_soa;
 
-/* Arguments of nvrx_scores: R score rows (ranks) x K kernel columns, row-major. */
+/* Arguments of nvrx_scores: R score rows (ranks) x K kernel columns, row-major.
+ * value_f64 selects the element type of med / avg / hist: 0 = float32 (statistics from
+ * the segment kernels, exact in f64), 1 = float64 (summaries handed in through the
+ * ReportGenerator API, whose MED/AVG are Python floats). */
 typedef struct nvrx_score_args {
     int64_t R, K;
+    int32_t value_f64;
     const int32_t* num;        /* [R][K] NUM; <= 0 means the kernel is absent on that rank */
-    const float* med;          /* [R][K] MED (us) */
-    const float* avg;          /* [R][K] AVG (us) */
+    const void* med;           /* [R][K] MED (us), float or double */
+    const void* avg;           /* [R][K] AVG (us), float or double */
     const uint8_t* col_valid;  /* [K] 0 = column filtered out ("ncclDev"), NULL = all valid */
     /* relative score reference (NULL = relative scores not computed) */
     const float* ref;          /* ref[ref_index ? ref_index[k] : k]; a value !(>= 0) (NaN, -1) = missing */
     const int32_t* ref_index;  /* [K] or NULL */
     /* individual score history (NULL = individual scores not computed); updated in place
      * to min(hist, MED) for every present kernel BEFORE scoring (reporting.py:469-474) */
-    float* hist;               /* hist[r*hist_stride + (hist_index ? hist_index[k] : k)] */
+    void* hist;                /* hist[r*hist_stride + (hist_index ? hist_index[k] : k)], float or double */
     const int32_t* hist_index; /* [K] or NULL */
     int64_t hist_stride;       /* per-row stride of hist; 0 => K */
     /* output: partial sums per row, 6 doubles:
@@ -110,11 +115,10 @@ int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const 
  * scratch: >= 2*K uint32 of device memory. */
 int nvrx_kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
                     uint32_t* scratch, void* stream);
-/* times[0:total] = -1; times[ids[i]] = (float)med_f32[i] (i < nk), then
- * times[ids_sec[j]] = (float)med_f64[j] (j < nsec): the _all_reduce_times pack. */
-int nvrx_pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
-                        const double* med_f64, const int32_t* ids_sec, int64_t nsec,
-                        float* times, int64_t total, void* stream);
+/* times[0:total] = -1; times[ids[i]] = float32(med[i]) for i < n: the float32 pack of
+ * _all_reduce_times (kernel ids first, section ids offset by the kernel count). */
+int nvrx_pack_min_times(const double* med, const int32_t* ids, int64_t n, float* times,
+                        int64_t total, void* stream);
 int nvrx_scores(const nvrx_score_args* args, void* stream);
 /* partials: [nshards][R][6], combined in shard order 0..nshards-1.
  * score = n > 0 ? sum(s*w)/sum(w) : NaN; round_f32 != 0 rounds to float32 (the
@@ -135,6 +139,13 @@ int nvrx_section_scores(const double* med, const uint8_t* present, int64_t R, in
                         double* hist, int32_t round_f32, double* out_rel, double* out_ind,
                         int32_t* err, void* stream);
 int nvrx_stragglers(const double* score, int64_t n, double thr, uint8_t* mask, void* stream);
+/* Statistics of section CPU timings (ms, float64): section s = vals[off[s] : off[s+1]]
+ * (off: [nsec+1], device).  MIN, MAX, MED = lower median s[(n-1)/2] (torch.median),
+ * AVG, STD = unbiased (NaN for n == 1), NUM -- Detector._get_section_summaries
+ * (straggler.py:171-197).  max_len bounds every section's length (<= 16384). */
+int nvrx_section_stats(const double* vals, const int64_t* off, int64_t nsec, int64_t max_len,
+                       int32_t* num, double* mn, double* mx, double* med, double* avg,
+                       double* sd, void* stream);
 
 /* ---------------------------------------------------------------- record streams */
 /* A record is one kernel execution: the slot of its composite kernel name and its

@@ -106,16 +106,13 @@ int nvrx_kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, 
     return hip_status(nvrx::kernel_ref(num, med, R, K, ref, scratch, S(stream)), "nvrx_kernel_ref");
 }
 
-int nvrx_pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
-                        const double* med_f64, const int32_t* ids_sec, int64_t nsec,
-                        float* times, int64_t total, void* stream) {
-    NVRX_CHECK_ARG(nk >= 0 && nsec >= 0 && total >= 0, "nvrx_pack_min_times: negative size");
+int nvrx_pack_min_times(const double* med, const int32_t* ids, int64_t n, float* times,
+                        int64_t total, void* stream) {
+    NVRX_CHECK_ARG(n >= 0 && total >= 0, "nvrx_pack_min_times: negative size");
     NVRX_CHECK_ARG(total == 0 || times, "nvrx_pack_min_times: null times");
-    NVRX_CHECK_ARG(nk == 0 || (med_f32 && ids), "nvrx_pack_min_times: null kernel inputs");
-    NVRX_CHECK_ARG(nsec == 0 || (med_f64 && ids_sec), "nvrx_pack_min_times: null section inputs");
-    NVRX_CHECK_ARG(nk + nsec <= total, "nvrx_pack_min_times: more entries than the tensor holds");
-    return hip_status(nvrx::pack_min_times(med_f32, ids, nk, med_f64, ids_sec, nsec, times, total,
-                                           S(stream)),
+    NVRX_CHECK_ARG(n == 0 || (med && ids), "nvrx_pack_min_times: null inputs");
+    NVRX_CHECK_ARG(n <= total, "nvrx_pack_min_times: more entries than the tensor holds");
+    return hip_status(nvrx::pack_min_times(med, ids, n, times, total, S(stream)),
                       "nvrx_pack_min_times");
 }
 
@@ -127,6 +124,7 @@ int nvrx_scores(const nvrx_score_args* a, void* stream) {
                    "nvrx_scores: null num/med/avg");
     NVRX_CHECK_ARG(!a->hist_index || a->hist_stride > 0,
                    "nvrx_scores: hist_index requires hist_stride");
+    NVRX_CHECK_ARG(a->value_f64 == 0 || a->value_f64 == 1, "nvrx_scores: bad value_f64");
     return hip_status(nvrx::scores(*a, S(stream)), "nvrx_scores");
 }
 
@@ -151,6 +149,18 @@ int nvrx_section_scores(const double* med, const uint8_t* present, int64_t R, in
     return hip_status(nvrx::section_scores(med, present, R, S_, ref_in, ref_index, ref_work, hist,
                                            round_f32, out_rel, out_ind, err, S(stream)),
                       "nvrx_section_scores");
+}
+
+int nvrx_section_stats(const double* vals, const int64_t* off, int64_t nsec, int64_t max_len,
+                       int32_t* num, double* mn, double* mx, double* med, double* avg,
+                       double* sd, void* stream) {
+    NVRX_CHECK_ARG(nsec >= 0 && max_len >= 0, "nvrx_section_stats: negative size");
+    NVRX_CHECK_ARG(nsec == 0 || (vals && off && num && mn && mx && med && avg && sd),
+                   "nvrx_section_stats: null array");
+    NVRX_CHECK_ARG(max_len <= 16384, "nvrx_section_stats: more than 16384 timings per section");
+    return hip_status(nvrx::section_stats(vals, off, nsec, max_len, num, mn, mx, med, avg, sd,
+                                          S(stream)),
+                      "nvrx_section_stats");
 }
 
 int nvrx_stragglers(const double* score, int64_t n, double thr, uint8_t* mask, void* stream) {

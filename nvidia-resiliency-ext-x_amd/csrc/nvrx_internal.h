@@ -16,9 +16,8 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
 
 hipError_t kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
                       uint32_t* scratch, hipStream_t st);
-hipError_t pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
-                          const double* med_f64, const int32_t* ids_sec, int64_t nsec,
-                          float* times, int64_t total, hipStream_t st);
+hipError_t pack_min_times(const double* med, const int32_t* ids, int64_t n, float* times,
+                          int64_t total, hipStream_t st);
 hipError_t scores(const nvrx_score_args& a, hipStream_t st);
 hipError_t finalize_scores(const double* partials, int64_t R, int64_t nshards, int round_f32,
                            double thr_rel, double thr_ind, double* gpu_rel, double* gpu_ind,
@@ -27,6 +26,9 @@ hipError_t section_scores(const double* med, const uint8_t* present, int64_t R, 
                           const float* ref_in, const int32_t* ref_index, float* ref_work,
                           double* hist, int round_f32, double* out_rel, double* out_ind,
                           int32_t* err, hipStream_t st);
+hipError_t section_stats(const double* vals, const int64_t* off, int64_t nsec, int64_t max_len,
+                         int32_t* num, double* mn, double* mx, double* med, double* avg,
+                         double* sd, hipStream_t st);
 hipError_t stragglers(const double* score, int64_t n, double thr, uint8_t* mask, hipStream_t st);
 
 #define NVRX_RECORDS_MAX_LDS (144 * 1024)

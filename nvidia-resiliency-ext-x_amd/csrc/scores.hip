@@ -90,26 +90,21 @@ __global__ void fill_f32_kernel(float* p, int64_t n, float v) {
          i += (int64_t)gridDim.x * blockDim.x)
         p[i] = v;
 }
-__global__ void pack_times_kernel(const float* med_f32, const int32_t* ids, int64_t nk,
-                                  const double* med_f64, const int32_t* ids_sec, int64_t nsec,
-                                  float* times) {
+__global__ void pack_times_kernel(const double* med, const int32_t* ids, int64_t n, float* times) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nk) times[ids[i]] = med_f32[i];
-    else if (i < nk + nsec) times[ids_sec[i - nk]] = (float)med_f64[i - nk];  // RN to float32
+    if (i < n) times[ids[i]] = (float)med[i];  // RN to float32, as the torch float32 store
 }
 
-hipError_t pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
-                          const double* med_f64, const int32_t* ids_sec, int64_t nsec,
-                          float* times, int64_t total, hipStream_t st) {
+hipError_t pack_min_times(const double* med, const int32_t* ids, int64_t n, float* times,
+                          int64_t total, hipStream_t st) {
     if (total > 0) {
         const int64_t gb = (total + 255) / 256;
         const unsigned g = (unsigned)(gb < 1024 ? gb : 1024);
         hipLaunchKernelGGL(fill_f32_kernel, dim3(g), dim3(256), 0, st, times, total, -1.0f);
     }
-    if (nk + nsec > 0) {
-        const unsigned g = (unsigned)((nk + nsec + 255) / 256);
-        hipLaunchKernelGGL(pack_times_kernel, dim3(g), dim3(256), 0, st, med_f32, ids, nk,
-                           med_f64, ids_sec, nsec, times);
+    if (n > 0) {
+        const unsigned g = (unsigned)((n + 255) / 256);
+        hipLaunchKernelGGL(pack_times_kernel, dim3(g), dim3(256), 0, st, med, ids, n, times);
     }
     return hipGetLastError();
 }
@@ -117,6 +112,10 @@ hipError_t pack_min_times(const float* med_f32, const int32_t* ids, int64_t nk,
 // ---------------------------------------------------------------------------
 // Per-row weighted score partials: one 64-lane wave per row.
 // ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T tmin(T a, T b) { return b < a ? b : a; }  // Python min(a, b)
+
+template <typename T>
 __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id();
@@ -129,18 +128,19 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
     double swr = 0.0, wr = 0.0, nr = 0.0, swi = 0.0, wi = 0.0, ni = 0.0;
     bool zero_med = false;
     const int32_t* num = a.num + r * K;
-    const float* med = a.med + r * K;
-    const float* avg = a.avg + r * K;
+    const T* med = (const T*)a.med + r * K;
+    const T* avg = (const T*)a.avg + r * K;
+    T* hist = (T*)a.hist;
     for (int64_t k = lane; k < K; k += 64) {
         if (a.col_valid && !a.col_valid[k]) continue;  // "ncclDev" filter (reporting.py:330-336)
         const int32_t nm = num[k];
         if (nm <= 0) continue;  // kernel not in this rank's summaries
-        const float mf = med[k];
-        const double m = (double)mf;
+        const T mt = med[k];
+        const double m = (double)mt;
         const double w = (double)nm * (double)avg[k];  // NUM * AVG (reporting.py:248)
         if (do_ind) {
-            float* hp = a.hist + r * hs + (a.hist_index ? a.hist_index[k] : k);
-            const float h = fminf(*hp, mf);  // min(hist, MED) (reporting.py:310)
+            T* hp = hist + r * hs + (a.hist_index ? a.hist_index[k] : k);
+            const T h = tmin(*hp, mt);  // min(hist, MED) (reporting.py:310)
             *hp = h;
             zero_med |= (m == 0.0);
             const double sc = (double)h / m;
@@ -183,7 +183,10 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
 hipError_t scores(const nvrx_score_args& a, hipStream_t st) {
     if (a.R <= 0) return hipSuccess;
     const unsigned g = (unsigned)((a.R + 3) / 4);
-    hipLaunchKernelGGL(scores_kernel, dim3(g), dim3(256), 0, st, a);
+    if (a.value_f64)
+        hipLaunchKernelGGL(scores_kernel<double>, dim3(g), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(scores_kernel<float>, dim3(g), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ class StatsSoA(ctypes.Structure):
 
 class ScoreArgs(ctypes.Structure):
     _fields_ = [
-        ("R", i64), ("K", i64),
+        ("R", i64), ("K", i64), ("value_f64", i32),
         ("num", P), ("med", P), ("avg", P), ("col_valid", P),
         ("ref", P), ("ref_index", P),
         ("hist", P), ("hist_index", P), ("hist_stride", i64),
@@ -69,11 +69,12 @@ SIGNATURES = {
     "nvrx_segment_stats_ragged": (ctypes.c_int, [P, P, P, i64, i64, i64, i32, i32,
                                                  ctypes.POINTER(StatsSoA), P]),
     "nvrx_kernel_ref": (ctypes.c_int, [P, P, i64, i64, P, P, P]),
-    "nvrx_pack_min_times": (ctypes.c_int, [P, P, i64, P, P, i64, P, i64, P]),
+    "nvrx_pack_min_times": (ctypes.c_int, [P, P, i64, P, i64, P]),
     "nvrx_scores": (ctypes.c_int, [ctypes.POINTER(ScoreArgs), P]),
     "nvrx_finalize_scores": (ctypes.c_int, [P, i64, i64, i32, f64, f64, P, P, P, P, P, P]),
     "nvrx_section_scores": (ctypes.c_int, [P, P, i64, i64, P, P, P, P, i32, P, P, P, P]),
     "nvrx_stragglers": (ctypes.c_int, [P, i64, f64, P, P]),
+    "nvrx_section_stats": (ctypes.c_int, [P, P, i64, i64, P, P, P, P, P, P, P]),
     "nvrx_records_bucket_capacity": (i64, [i64, i64, i64]),
     "nvrx_records_bucket": (ctypes.c_int, [P, P, i64, i64, i64, P, P, P, P, P]),
     "nvrx_records_max_slots": (i64, []),

@@ -1,0 +1,193 @@
+"""Kernel-duration capture manager (drop-in for straggler/cupti.py:19-95).
+
+``KernelProfiler`` replaces the pybind11 ``nvrx_cupti_module.CuptiProfiler``
+(cupti_module_py.cpp:33-54) with the nvrx_profiler handle of libnvrx_hip.so: records are
+kept as a device-resident log in HBM and reduced to per-kernel statistics by the HIP
+kernels at get_stats time (only the last ``statsMaxLenPerKernel`` records of every kernel
+count, as the reference's rings keep them).  Records enter through ``push`` (and, when
+available, the rocprofiler-sdk kernel-dispatch capture).
+
+``CuptiManager`` keeps the reference's thread-safe, refcounted start/stop semantics.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Dict, Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+from .summaries import KernelSummaries
+
+
+class KernelStats:
+    """Per-kernel statistics as the reference module exposes them (CuptiProfiler.h:39-45)."""
+
+    __slots__ = ("num_calls", "min", "max", "median", "avg", "stddev")
+
+    def __init__(self, num_calls=0, mn=float("nan"), mx=float("nan"), median=float("nan"),
+                 avg=float("nan"), stddev=float("nan")):
+        self.num_calls, self.min, self.max = num_calls, mn, mx
+        self.median, self.avg, self.stddev = median, avg, stddev
+
+    def __str__(self):
+        return (f" num calls: {self.num_calls}, min: {self.min}, max: {self.max}, median: "
+                f"{self.median}, avg: {self.avg}, stddev: {self.stddev}")
+
+
+class KernelProfiler:
+    """nvrx_cupti_module.CuptiProfiler(bufferSize, numBuffers, statsMaxLenPerKernel)."""
+
+    def __init__(self, bufferSize: int = 1024 * 1024 * 8, numBuffers: int = 8,
+                 statsMaxLenPerKernel: int = 1024, device: Optional[int] = None,
+                 exact: bool = True):
+        if device is None:
+            import torch
+
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        cfg = N.ProfilerConfig(bufferSize, numBuffers, statsMaxLenPerKernel, int(device),
+                               N.NVRX_STATS_EXACT if exact else N.NVRX_STATS_FAST)
+        h = ctypes.c_void_p()
+        N.check(N.lib().nvrx_profiler_create(ctypes.byref(cfg), ctypes.byref(h)),
+                "CuptiProfiler")
+        self._h = h
+        self._slot_of: Dict[str, int] = {}
+        self._names: list = []
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.lib().nvrx_profiler_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def close(self):
+        self.__del__()
+
+    def initialize(self):
+        N.call("nvrx_profiler_initialize", self._h)
+
+    def shutdown(self):
+        N.call("nvrx_profiler_shutdown", self._h)
+
+    def start(self):
+        N.call("nvrx_profiler_start", self._h)
+
+    def stop(self):
+        N.call("nvrx_profiler_stop", self._h)
+
+    def reset(self):
+        N.call("nvrx_profiler_reset", self._h)
+
+    def register_kernel(self, name: str) -> int:
+        s = self._slot_of.get(name)
+        if s is None:
+            out = ctypes.c_uint32()
+            N.call("nvrx_profiler_register_kernel", self._h, name.encode(), ctypes.byref(out))
+            s = int(out.value)
+            self._slot_of[name] = s
+            while len(self._names) <= s:
+                self._names.append(None)
+            self._names[s] = name
+        return s
+
+    def push(self, name: str, durations_ns: Iterable[int]) -> None:
+        """Append kernel executions of `name` (durations in ns, push order)."""
+        d = np.asarray(list(durations_ns) if not isinstance(durations_ns, np.ndarray)
+                       else durations_ns, dtype=np.uint64)
+        self.push_slots(np.full(d.size, self.register_kernel(name), np.uint32), d)
+
+    def push_slots(self, slots: np.ndarray, durations_ns: np.ndarray) -> None:
+        recs = np.empty((len(slots), 2), dtype=np.uint32)
+        recs[:, 0] = slots
+        recs[:, 1] = np.minimum(np.asarray(durations_ns, dtype=np.uint64), 0xFFFFFFFF)
+        N.call("nvrx_profiler_push", self._h, recs.ctypes.data, len(slots))
+
+    def get_stats_columns(self) -> KernelSummaries:
+        """Per-kernel statistics (HIP) as columns, sorted by composite kernel name."""
+        L = N.lib()
+        count = ctypes.c_int64()
+        N.call("nvrx_profiler_get_stats", self._h, 0, ctypes.byref(count), None, None, None,
+               None, None, None, None)
+        n = int(count.value)
+        slots = np.empty(n, np.uint32)
+        num = np.empty(n, np.int32)
+        cols = [np.empty(n, np.float32) for _ in range(5)]
+        p = lambda a: a.ctypes.data  # noqa: E731
+        N.check(L.nvrx_profiler_get_stats(self._h, n, ctypes.byref(count), p(slots), p(num),
+                                          *(p(c) for c in cols)), "get_stats")
+        names = [self._names[s] for s in slots]
+        return KernelSummaries(names, num, *cols)
+
+    def get_stats(self) -> Dict[str, KernelStats]:
+        ks = self.get_stats_columns()
+        return {n: KernelStats(int(ks.num[i]), float(ks.min[i]), float(ks.max[i]),
+                               float(ks.med[i]), float(ks.avg[i]), float(ks.std[i]))
+                for i, n in enumerate(ks.names)}
+
+
+class CuptiManager:
+    """Thread-safe access to the profiler with a usage counter of active profiling runs."""
+
+    def __init__(self, bufferSize=1_000_000, numBuffers=8, statsMaxLenPerKernel=4096):
+        self.cupti_ext = KernelProfiler(bufferSize=bufferSize, numBuffers=numBuffers,
+                                        statsMaxLenPerKernel=statsMaxLenPerKernel)
+        self.is_initialized = False
+        self.started_cnt = 0
+        self.lock = threading.Lock()
+
+    def _ensure_initialized(self):
+        if not self.is_initialized:
+            raise RuntimeError("CuptiManager was not initialized")
+
+    def initialize(self):
+        with self.lock:
+            self.cupti_ext.initialize()
+            self.is_initialized = True
+
+    def shutdown(self):
+        with self.lock:
+            self.cupti_ext.shutdown()
+            self.is_initialized = False
+            self.started_cnt = 0
+            self.cupti_ext.close()
+
+    def start_profiling(self):
+        with self.lock:
+            self._ensure_initialized()
+            if self.started_cnt == 0:
+                self.cupti_ext.start()
+            self.started_cnt += 1
+
+    def stop_profiling(self):
+        with self.lock:
+            self._ensure_initialized()
+            if self.started_cnt > 0:
+                self.started_cnt -= 1
+                if self.started_cnt == 0:
+                    self.cupti_ext.stop()
+            else:
+                raise RuntimeError("No active profiling run.")
+
+    def get_results(self):
+        with self.lock:
+            self._ensure_initialized()
+            return self.cupti_ext.get_stats().copy()
+
+    def get_results_columns(self) -> KernelSummaries:
+        with self.lock:
+            self._ensure_initialized()
+            return self.cupti_ext.get_stats_columns()
+
+    def reset_results(self):
+        with self.lock:
+            self._ensure_initialized()
+            self.cupti_ext.reset()
+
+    def push(self, name: str, durations_ns: Sequence[int]):
+        """Feed kernel executions (e.g. from an external tracer) into the active run."""
+        with self.lock:
+            self.cupti_ext.push(name, durations_ns)

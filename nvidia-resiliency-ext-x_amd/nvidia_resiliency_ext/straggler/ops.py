@@ -100,15 +100,13 @@ def kernel_ref(num: torch.Tensor, med: torch.Tensor, ref: Optional[torch.Tensor]
     return ref
 
 
-def pack_min_times(med_f32: torch.Tensor, ids: torch.Tensor, med_f64: torch.Tensor,
-                   ids_sec: torch.Tensor, total: int, out: Optional[torch.Tensor] = None,
-                   stream=None) -> torch.Tensor:
-    dev = med_f32.device
+def pack_min_times(med: torch.Tensor, ids: torch.Tensor, total: int,
+                   out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+    """times = -1; times[ids[i]] = float32(med[i]): the _all_reduce_times pack (reporting.py:269-279)."""
     if out is None:
-        out = torch.empty(total, dtype=torch.float32, device=dev)
-    N.call("nvrx_pack_min_times", med_f32.data_ptr(), ids.data_ptr(), med_f32.numel(),
-           med_f64.data_ptr(), ids_sec.data_ptr(), med_f64.numel(), out.data_ptr(), total,
-           _stream(stream))
+        out = torch.empty(max(total, 1), dtype=torch.float32, device=med.device)
+    N.call("nvrx_pack_min_times", med.data_ptr(), ids.data_ptr(), med.numel(), out.data_ptr(),
+           total, _stream(stream))
     return out
 
 
@@ -118,7 +116,10 @@ def scores(num, med, avg, *, col_valid=None, ref=None, ref_index=None, hist=None
     R, K = med.shape
     if partials is None:
         partials = torch.empty((R, 6), dtype=torch.float64, device=med.device)
-    a = N.ScoreArgs(R, K, num.data_ptr(), med.data_ptr(), avg.data_ptr(), N.ptr(col_valid),
+    f64 = med.dtype == torch.float64
+    if avg.dtype != med.dtype or (hist is not None and hist.dtype != med.dtype):
+        raise TypeError("med, avg and hist must share one float dtype")
+    a = N.ScoreArgs(R, K, int(f64), num.data_ptr(), med.data_ptr(), avg.data_ptr(), N.ptr(col_valid),
                     N.ptr(ref), N.ptr(ref_index), N.ptr(hist), N.ptr(hist_index), hist_stride,
                     partials.data_ptr(), N.ptr(err))
     N.call("nvrx_scores", ctypes.byref(a), _stream(stream))
@@ -150,6 +151,17 @@ def section_scores(med: torch.Tensor, present: torch.Tensor, *, ref_in=None, ref
            N.ptr(ref_index), N.ptr(ref_work), N.ptr(hist), int(round_f32), N.ptr(out_rel),
            N.ptr(out_ind), N.ptr(err), _stream(stream))
     return out_rel, out_ind
+
+
+def section_stats(values: torch.Tensor, off: torch.Tensor, max_len: int, stream=None):
+    """Per-section (num, min, max, med, avg, std) of float64 ms timings (straggler.py:171-197)."""
+    nsec = off.numel() - 1
+    dev = values.device
+    num = torch.empty(nsec, dtype=torch.int32, device=dev)
+    out = torch.empty((5, nsec), dtype=torch.float64, device=dev)
+    N.call("nvrx_section_stats", values.data_ptr(), off.data_ptr(), nsec, max_len, num.data_ptr(),
+           *(out[i].data_ptr() for i in range(5)), _stream(stream))
+    return num, out
 
 
 def stragglers(score: torch.Tensor, thr: float, out: Optional[torch.Tensor] = None, stream=None):

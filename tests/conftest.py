@@ -6,7 +6,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "nvidia-resiliency-ext-x_amd")
 ORACLE = os.path.join(ROOT, "oracle")
-for p in (PKG, ORACLE, ROOT):
+for p in (PKG, ORACLE, ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
