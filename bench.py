@@ -92,7 +92,8 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True)
         rep.compute_stats(ns, s_push)
         if time_kernel:
             ev[i][1].record()
-        res = rep.finalize(rep.compute_partials())
+        rep.compute_scores()
+        res = rep.land()
     barrier(world)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if time_kernel else None

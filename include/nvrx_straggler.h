@@ -79,15 +79,24 @@ typedef struct nvrx_score_args {
     /* relative score reference (NULL = relative scores not computed) */
     const float* ref;          /* ref[ref_index ? ref_index[k] : k]; a value !(>= 0) (NaN, -1) = missing */
     const int32_t* ref_index;  /* [K] or NULL */
+    const uint32_t* ref_missing; /* [K] or NULL: nonzero => reference missing (NaN) */
     /* individual score history (NULL = individual scores not computed); updated in place
      * to min(hist, MED) for every present kernel BEFORE scoring (reporting.py:469-474) */
     void* hist;                /* hist[r*hist_stride + (hist_index ? hist_index[k] : k)], float or double */
     const int32_t* hist_index; /* [K] or NULL */
     int64_t hist_stride;       /* per-row stride of hist; 0 => K */
-    /* output: partial sums per row, 6 doubles:
+    /* output: partial sums per row, 6 doubles (NULL allowed when finalizing in place):
      * {sum s*w (rel), sum w (rel), n (rel), sum s*w (ind), sum w (ind), n (ind)} */
     double* partials;          /* [R][6] */
-    int32_t* err;              /* [1] device flags |= 1 when some MED == 0 (ZeroDivisionError) */
+    int32_t* err;              /* [1] device flags |= 1 when some MED == 0, |= 2 when a score's
+                                  total weight is 0 (ZeroDivisionError) */
+    /* optional in-kernel finalize (single shard), as nvrx_finalize_scores: any may be NULL */
+    int32_t round_f32;
+    double thr_rel, thr_ind;
+    double* gpu_rel;
+    double* gpu_ind;
+    uint8_t* strag_rel;
+    uint8_t* strag_ind;
 } nvrx_score_args;
 
 /* ---------------------------------------------------------------- library */
@@ -98,10 +107,16 @@ int nvrx_sync(void* stream);                   /* synchronous: waits for `stream
 
 /* ---------------------------------------------------------------- statistics */
 /* Segment s = ns[s*seg_stride + seg_begin : + seg_len] (uint32 ns durations); the
- * last min(seg_len, cap) samples are retained (cap <= 0: all).  out->* are [nseg]. */
+ * last min(seg_len, cap) samples are retained (cap <= 0: all).  out->* are [nseg].
+ * col_ref (optional, [2*ncols] uint32): segments form a [nseg/ncols][ncols] rank x kernel
+ * matrix; the call also produces the per-kernel relative reference of _all_reduce_times
+ * (reporting.py:255-296): col_ref[c] = float bits of min over rows of MED, col_ref[ncols+c]
+ * != 0 when some row has no sample of c (=> NaN).  Feed (float*)col_ref as nvrx_score_args
+ * .ref and col_ref + ncols as .ref_missing. */
 int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
                                int64_t seg_begin, int64_t seg_len, int64_t cap, int32_t mode,
-                               const nvrx_stats_soa* out, void* stream);
+                               const nvrx_stats_soa* out, uint32_t* col_ref, int64_t ncols,
+                               void* stream);
 /* Segment s = ns[seg_off[s] : seg_off[s] + seg_len[s]] (device arrays; seg_len NULL:
  * seg_off has nseg+1 entries and segment s ends at seg_off[s+1]); max_len bounds every
  * segment length (host-known); aligned16 != 0 promises every retained run starts on a

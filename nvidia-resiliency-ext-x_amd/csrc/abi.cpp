@@ -59,7 +59,8 @@ int nvrx_sync(void* stream) { return hip_status(hipStreamSynchronize(S(stream)),
 // ------------------------------------------------------------------ statistics
 int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
                                int64_t seg_begin, int64_t seg_len, int64_t cap, int32_t mode,
-                               const nvrx_stats_soa* out, void* stream) {
+                               const nvrx_stats_soa* out, uint32_t* col_ref, int64_t ncols,
+                               void* stream) {
     NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
                    "nvrx_segment_stats_strided: null output array");
     NVRX_CHECK_ARG(nseg >= 0 && seg_len >= 0 && seg_begin >= 0 && seg_stride >= 0,
@@ -73,8 +74,10 @@ int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_str
     NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT,
                    "nvrx_segment_stats_strided: retained segment longer than NVRX_MAX_SEGMENT");
     NVRX_CHECK_ARG(nseg < (int64_t)1 << 33, "nvrx_segment_stats_strided: too many segments");
+    NVRX_CHECK_ARG(!col_ref || (ncols > 0 && nseg % ncols == 0),
+                   "nvrx_segment_stats_strided: col_ref needs ncols > 0 dividing nseg");
     return hip_status(nvrx::segment_stats_strided(ns, nseg, seg_stride, seg_begin, seg_len, cap,
-                                                  mode, *out, S(stream)),
+                                                  mode, *out, col_ref, ncols, S(stream)),
                       "nvrx_segment_stats_strided");
 }
 
@@ -119,7 +122,9 @@ int nvrx_pack_min_times(const double* med, const int32_t* ids, int64_t n, float*
 int nvrx_scores(const nvrx_score_args* a, void* stream) {
     NVRX_CHECK_ARG(a, "nvrx_scores: null args");
     NVRX_CHECK_ARG(a->R >= 0 && a->K >= 0, "nvrx_scores: negative size");
-    NVRX_CHECK_ARG(a->R == 0 || a->partials, "nvrx_scores: null partials");
+    NVRX_CHECK_ARG(a->R == 0 || a->partials || a->gpu_rel || a->gpu_ind || a->strag_rel ||
+                       a->strag_ind,
+                   "nvrx_scores: no output (partials or finalized scores)");
     NVRX_CHECK_ARG(a->R == 0 || a->K == 0 || (a->num && a->med && a->avg),
                    "nvrx_scores: null num/med/avg");
     NVRX_CHECK_ARG(!a->hist_index || a->hist_stride > 0,

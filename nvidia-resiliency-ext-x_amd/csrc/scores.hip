@@ -115,12 +115,27 @@ hipError_t pack_min_times(const double* med, const int32_t* ids, int64_t n, floa
 template <typename T>
 __device__ __forceinline__ T tmin(T a, T b) { return b < a ? b : a; }  // Python min(a, b)
 
+// score = n > 0 ? sum(s*w)/sum(w) : NaN (reporting.py:251-253); returns true when the
+// total weight is 0 (Python raises ZeroDivisionError there).
+__device__ __forceinline__ bool finish(double sw, double w, double n, double& out) {
+    out = __builtin_nan("");
+    if (n > 0.0) {
+        out = sw / w;
+        return w == 0.0;
+    }
+    return false;
+}
+
+// One 256-thread workgroup per row (rank): lanes stride over the kernels, each wave
+// reduces with DPP, the 4 wave results are added in wave order (deterministic).
 template <typename T>
 __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = lane_id();
-    const int64_t r = (int64_t)blockIdx.x * 4 + wave;
-    if (r >= a.R) return;
+    __shared__ double red[4][6];
+    __shared__ int zflag[4];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & 63;
+    const int64_t r = blockIdx.x;
     const int64_t K = a.K;
     const int64_t hs = a.hist_stride > 0 ? a.hist_stride : K;
     const bool do_rel = a.ref != nullptr;
@@ -131,7 +146,7 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
     const T* med = (const T*)a.med + r * K;
     const T* avg = (const T*)a.avg + r * K;
     T* hist = (T*)a.hist;
-    for (int64_t k = lane; k < K; k += 64) {
+    for (int64_t k = tid; k < K; k += 256) {
         if (a.col_valid && !a.col_valid[k]) continue;  // "ncclDev" filter (reporting.py:330-336)
         const int32_t nm = num[k];
         if (nm <= 0) continue;  // kernel not in this rank's summaries
@@ -150,8 +165,10 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
             ni += 1.0;
         }
         if (do_rel) {
-            const float rf = a.ref[a.ref_index ? a.ref_index[k] : k];
-            if (rf >= 0.0f) {  // -1 sentinel / NaN => no reference (reporting.py:290, 244-245)
+            const int64_t ri = a.ref_index ? a.ref_index[k] : k;
+            const float rf = a.ref[ri];
+            const bool missing = a.ref_missing && a.ref_missing[ri];
+            if (rf >= 0.0f && !missing) {  // -1 sentinel / NaN => no reference (reporting.py:290, 244-245)
                 zero_med |= (m == 0.0);
                 const double sc = (double)rf / m;
                 const double t = sc * w;
@@ -169,20 +186,46 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
     ni = wave_sum_f64(ni);
     const bool anyzero = __ballot(zero_med) != 0;
     if (lane == 0) {
-        double* o = a.partials + r * 6;
-        o[0] = swr;
-        o[1] = wr;
-        o[2] = nr;
-        o[3] = swi;
-        o[4] = wi;
-        o[5] = ni;
-        if (anyzero && a.err) atomicOr(a.err, 1);
+        red[wave][0] = swr;
+        red[wave][1] = wr;
+        red[wave][2] = nr;
+        red[wave][3] = swi;
+        red[wave][4] = wi;
+        red[wave][5] = ni;
+        zflag[wave] = anyzero;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double p[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) p[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+        int errbits = (zflag[0] | zflag[1] | zflag[2] | zflag[3]) ? 1 : 0;
+        if (a.partials) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) a.partials[r * 6 + i] = p[i];
+        }
+        if (a.gpu_rel || a.gpu_ind || a.strag_rel || a.strag_ind) {
+            double sr, si;
+            bool zw = finish(p[0], p[1], p[2], sr);
+            zw |= finish(p[3], p[4], p[5], si);
+            if (zw) errbits |= 2;
+            if (a.round_f32) {
+                sr = (double)(float)sr;
+                si = (double)(float)si;
+            }
+            if (a.gpu_rel) a.gpu_rel[r] = sr;
+            if (a.gpu_ind) a.gpu_ind[r] = si;
+            if (a.strag_rel) a.strag_rel[r] = sr < a.thr_rel;  // NaN compares false
+            if (a.strag_ind) a.strag_ind[r] = si < a.thr_ind;
+        }
+        if (errbits && a.err) atomicOr(a.err, errbits);
     }
 }
 
 hipError_t scores(const nvrx_score_args& a, hipStream_t st) {
     if (a.R <= 0) return hipSuccess;
-    const unsigned g = (unsigned)((a.R + 3) / 4);
+    if (a.R > 0x7FFFFFFF) return hipErrorInvalidValue;
+    const unsigned g = (unsigned)a.R;
     if (a.value_f64)
         hipLaunchKernelGGL(scores_kernel<double>, dim3(g), dim3(256), 0, st, a);
     else

@@ -55,6 +55,22 @@ struct RaggedSegs {  // segment s = base[off[s] : off[s] + len[s]] (len NULL: of
     }
 };
 
+// Optional fused per-column reference (segment s = row s / ncols, column s % ncols):
+// minbits[c] = atomicMin of the float bits of MED (non-negative floats order like their
+// bit patterns), missing[c] |= 1 for an empty segment -- _all_reduce_times'
+// MIN-over-ranks with the -1 => NaN rule (reporting.py:255-296), done in the epilogue.
+struct ColRef {
+    uint32_t* minbits;
+    uint32_t* missing;
+    int64_t ncols;
+    __device__ __forceinline__ void add(int64_t s, float med) const {
+        if (minbits) atomicMin(&minbits[s % ncols], __float_as_uint(med));
+    }
+    __device__ __forceinline__ void miss(int64_t s) const {
+        if (minbits) atomicOr(&missing[s % ncols], 1u);
+    }
+};
+
 __device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) {
     // KernelStats() default: num_calls 0, every float NaN (CuptiProfiler.h:39-45)
     const float q = __builtin_nanf("");
@@ -136,7 +152,7 @@ struct OccV {  // the masked PL=128 variant gets the whole 256-register budget
 // 16-byte boundary, so no lane needs masking.  !FULL: per-element masks (branch-free).
 template <int PL, bool FULL, class Segs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OccV<PL, FULL>::W)))
-void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out) {
+void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
     constexpr int NV = PL / 4;
     constexpr int NB = Bins<PL>::NB;
     constexpr int LOGNB = Bins<PL>::LOG;
@@ -153,7 +169,10 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out) {
     int n;
     segs.get(s, p, n);
     if (n <= 0) {
-        if (lane == 0) write_empty(out, s);
+        if (lane == 0) {
+            write_empty(out, s);
+            cr.miss(s);
+        }
         return;
     }
 
@@ -314,12 +333,13 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out) {
         out.min[s] = ns_to_us(mn);
         out.max[s] = ns_to_us(mx);
         const float f0 = ns_to_us(mn + d0);
-        if (n & 1) {
-            out.med[s] = f0;
-        } else {
+        float med = f0;
+        if (!(n & 1)) {
             const float f1 = ns_to_us(mn + d1);
-            out.med[s] = (f0 + f1) / 2;  // f32 add, exact halving (CuptiProfiler.cpp:58)
+            med = (f0 + f1) / 2;  // f32 add, exact halving (CuptiProfiler.cpp:58)
         }
+        out.med[s] = med;
+        cr.add(s, med);
         const double dn = (double)n;
         const double mean_d = sd / dn;
         out.avg[s] = (float)(((double)mn + mean_d) / 1000.0);
@@ -334,7 +354,7 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out) {
 // ---------------------------------------------------------------------------
 template <int NMAX, class Segs>
 __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t nseg,
-                                                              nvrx_stats_soa out) {
+                                                              nvrx_stats_soa out, ColRef cr) {
     __shared__ __attribute__((aligned(16))) float sbuf[NMAX];
     const int64_t s = blockIdx.x;
     if (s >= nseg) return;
@@ -342,7 +362,10 @@ __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t
     int n;
     segs.get(s, p, n);
     if (n <= 0) {
-        if (threadIdx.x == 0) write_empty(out, s);
+        if (threadIdx.x == 0) {
+            write_empty(out, s);
+            cr.miss(s);
+        }
         return;
     }
     int np2 = 1;
@@ -389,6 +412,7 @@ __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t
         out.min[s] = mnv;
         out.max[s] = mxv;
         out.med[s] = med;
+        cr.add(s, med);
         out.avg[s] = avg;
         out.std[s] = sd;
     }
@@ -399,31 +423,31 @@ __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t
 // ---------------------------------------------------------------------------
 template <int PL, class Segs>
 static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
-                      hipStream_t st) {
+                      const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
     if (full)
-        hipLaunchKernelGGL((seg_stats_fast_kernel<PL, true, Segs>), grid, block, 0, st, segs, nseg, out);
+        hipLaunchKernelGGL((seg_stats_fast_kernel<PL, true, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else
-        hipLaunchKernelGGL((seg_stats_fast_kernel<PL, false, Segs>), grid, block, 0, st, segs, nseg, out);
+        hipLaunchKernelGGL((seg_stats_fast_kernel<PL, false, Segs>), grid, block, 0, st, segs, nseg, out, cr);
 }
 
 // need = samples + alignment slack a wave must hold; picks the smallest PL.  `full`
 // (every segment exactly 64*PL samples, 16-B aligned) selects the unmasked variant.
 template <class Segs>
 static hipError_t launch_fast(const Segs& segs, int64_t nseg, int64_t need, int64_t exact_len,
-                              const nvrx_stats_soa& out, hipStream_t st) {
+                              const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
     if (need <= 64 * 4)
-        launch_pl<4>(segs, nseg, exact_len == 64 * 4, out, st);
+        launch_pl<4>(segs, nseg, exact_len == 64 * 4, out, cr, st);
     else if (need <= 64 * 8)
-        launch_pl<8>(segs, nseg, exact_len == 64 * 8, out, st);
+        launch_pl<8>(segs, nseg, exact_len == 64 * 8, out, cr, st);
     else if (need <= 64 * 16)
-        launch_pl<16>(segs, nseg, exact_len == 64 * 16, out, st);
+        launch_pl<16>(segs, nseg, exact_len == 64 * 16, out, cr, st);
     else if (need <= 64 * 32)
-        launch_pl<32>(segs, nseg, exact_len == 64 * 32, out, st);
+        launch_pl<32>(segs, nseg, exact_len == 64 * 32, out, cr, st);
     else if (need <= 64 * 64)
-        launch_pl<64>(segs, nseg, exact_len == 64 * 64, out, st);
+        launch_pl<64>(segs, nseg, exact_len == 64 * 64, out, cr, st);
     else if (need <= 64 * 128)
-        launch_pl<128>(segs, nseg, exact_len == 64 * 128, out, st);
+        launch_pl<128>(segs, nseg, exact_len == 64 * 128, out, cr, st);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -431,14 +455,14 @@ static hipError_t launch_fast(const Segs& segs, int64_t nseg, int64_t need, int6
 
 template <class Segs>
 static hipError_t launch_exact(const Segs& segs, int64_t nseg, int64_t max_len,
-                               const nvrx_stats_soa& out, hipStream_t st) {
+                               const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)nseg), block(256);
     if (max_len <= 1024)
-        hipLaunchKernelGGL((seg_stats_exact_kernel<1024, Segs>), grid, block, 0, st, segs, nseg, out);
+        hipLaunchKernelGGL((seg_stats_exact_kernel<1024, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else if (max_len <= 8192)
-        hipLaunchKernelGGL((seg_stats_exact_kernel<8192, Segs>), grid, block, 0, st, segs, nseg, out);
+        hipLaunchKernelGGL((seg_stats_exact_kernel<8192, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else if (max_len <= NVRX_MAX_SEGMENT)
-        hipLaunchKernelGGL((seg_stats_exact_kernel<NVRX_MAX_SEGMENT, Segs>), grid, block, 0, st, segs, nseg, out);
+        hipLaunchKernelGGL((seg_stats_exact_kernel<NVRX_MAX_SEGMENT, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -449,7 +473,16 @@ static hipError_t launch_exact(const Segs& segs, int64_t nseg, int64_t max_len,
 // or misaligned-and-full segments go to the EXACT kernel (bit-exact, slower).
 hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
                                  int64_t seg_begin, int64_t seg_len, int64_t cap, int mode,
-                                 const nvrx_stats_soa& out, hipStream_t st) {
+                                 const nvrx_stats_soa& out, uint32_t* col_ref, int64_t ncols,
+                                 hipStream_t st) {
+    ColRef cr{nullptr, nullptr, 1};
+    if (col_ref && ncols > 0) {
+        cr = ColRef{col_ref, col_ref + ncols, ncols};
+        hipError_t e = hipMemsetD32Async((hipDeviceptr_t)col_ref, 0x7F800000, (size_t)ncols, st);
+        if (e == hipSuccess)
+            e = hipMemsetD32Async((hipDeviceptr_t)(col_ref + ncols), 0, (size_t)ncols, st);
+        if (e != hipSuccess) return e;
+    }
     if (nseg <= 0) return hipSuccess;
     StridedSegs segs{ns, seg_stride, seg_begin, seg_len, cap};
     const int64_t keep = (cap > 0 && seg_len > cap) ? cap : seg_len;
@@ -457,9 +490,9 @@ hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_s
     const bool aligned = ((seg_stride % 4) == 0) &&
                          ((((uintptr_t)(ns + seg_begin + (seg_len - keep))) & 15) == 0);
     const int64_t need = aligned ? keep : keep + 3;
-    if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, st);
+    if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
     // every strided segment has the same length and (aligned) phase
-    return launch_fast(segs, nseg, need, aligned ? keep : -1, out, st);
+    return launch_fast(segs, nseg, need, aligned ? keep : -1, out, cr, st);
 }
 
 hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
@@ -470,8 +503,9 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
     if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
     const int64_t need = aligned16 ? keep : keep + 3;
-    if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, st);
-    return launch_fast(segs, nseg, need, -1, out, st);  // lengths vary: masked variant
+    const ColRef cr{nullptr, nullptr, 1};
+    if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
+    return launch_fast(segs, nseg, need, -1, out, cr, st);  // lengths vary: masked variant
 }
 
 }  // namespace nvrx

@@ -41,9 +41,11 @@ class ScoreArgs(ctypes.Structure):
     _fields_ = [
         ("R", i64), ("K", i64), ("value_f64", i32),
         ("num", P), ("med", P), ("avg", P), ("col_valid", P),
-        ("ref", P), ("ref_index", P),
+        ("ref", P), ("ref_index", P), ("ref_missing", P),
         ("hist", P), ("hist_index", P), ("hist_stride", i64),
         ("partials", P), ("err", P),
+        ("round_f32", i32), ("thr_rel", f64), ("thr_ind", f64),
+        ("gpu_rel", P), ("gpu_ind", P), ("strag_rel", P), ("strag_ind", P),
     ]
 
 
@@ -65,7 +67,7 @@ SIGNATURES = {
     "nvrx_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "nvrx_sync": (ctypes.c_int, [P]),
     "nvrx_segment_stats_strided": (ctypes.c_int, [P, i64, i64, i64, i64, i64, i32,
-                                                  ctypes.POINTER(StatsSoA), P]),
+                                                  ctypes.POINTER(StatsSoA), P, i64, P]),
     "nvrx_segment_stats_ragged": (ctypes.c_int, [P, P, P, i64, i64, i64, i32, i32,
                                                  ctypes.POINTER(StatsSoA), P]),
     "nvrx_kernel_ref": (ctypes.c_int, [P, P, i64, i64, P, P, P]),

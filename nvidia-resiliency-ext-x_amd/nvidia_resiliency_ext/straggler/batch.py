@@ -48,67 +48,89 @@ class MatrixReporter:
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         d = self.device
         self.world = 1
+        self.gloo = False
         if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
             self.world = torch.distributed.get_world_size(group)
+            self.gloo = torch.distributed.get_backend(group) == torch.distributed.Backend.GLOO
         self.stats = ops.SegmentStats.empty(R * K, d)
         self.col_valid = col_valid
-        self.ref = torch.empty(K, dtype=torch.float32, device=d)
-        self.ref_scratch = torch.empty(2 * max(K, 1), dtype=torch.int32, device=d)
+        # per-kernel reference, produced by the stats kernel's epilogue: [min bits | missing]
+        self.col_ref = torch.empty(2 * max(K, 1), dtype=torch.int32, device=d)
         self.hist = torch.full((R, K), float("inf"), dtype=torch.float32, device=d) if individual else None
         self.partials = torch.empty((R, 6), dtype=torch.float64, device=d)
         self.gathered = (torch.empty((self.world, R, 6), dtype=torch.float64, device=d)
                          if self.world > 1 else None)
-        self.err = torch.zeros(1, dtype=torch.int32, device=d)
-        # pinned host landing buffers for the scores / straggler masks
-        self.h_scores = torch.empty((2, R), dtype=torch.float64, pin_memory=True)
-        self.h_masks = torch.empty((2, R), dtype=torch.uint8, pin_memory=True)
-        self.h_err = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        # one packed result buffer -> one device-to-host copy per report:
+        # [gpu_rel f64 R][gpu_ind f64 R][strag_rel u8 R][strag_ind u8 R][pad][err i32]
+        self._e = (18 * R + 7) // 8 * 8
+        nbytes = self._e + 8
+        self.out = torch.zeros(nbytes, dtype=torch.uint8, device=d)
+        self.h_out = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.views = dict(gpu_rel=self.out[0:8 * R].view(torch.float64),
+                          gpu_ind=self.out[8 * R:16 * R].view(torch.float64),
+                          strag_rel=self.out[16 * R:17 * R], strag_ind=self.out[17 * R:18 * R])
+        self.err = self.out[self._e:self._e + 4].view(torch.int32)
 
     def reset_history(self):
         if self.hist is not None:
             self.hist.fill_(float("inf"))
 
-    # -- the three device phases, separately callable (bench times the stats kernel) --
+    # -- device phases, separately callable (bench times the stats kernel) --
     def compute_stats(self, ns: torch.Tensor, s_push: int) -> ops.SegmentStats:
         return ops.segment_stats_strided(ns.view(-1), self.R * self.K, s_push, 0, s_push,
-                                         cap=self.cap, mode=self.mode, out=self.stats)
+                                         cap=self.cap, mode=self.mode, out=self.stats,
+                                         col_ref=self.col_ref if self.relative else None,
+                                         ncols=self.K)
 
-    def compute_partials(self) -> torch.Tensor:
+    def _outputs(self):
+        v = self.views
+        return dict(gpu_rel=v["gpu_rel"] if self.relative else None,
+                    gpu_ind=v["gpu_ind"] if self.individual else None,
+                    strag_rel=v["strag_rel"] if self.relative else None,
+                    strag_ind=v["strag_ind"] if self.individual else None,
+                    thr_rel=self.thr_rel, thr_ind=self.thr_ind, round_f32=self.round_f32)
+
+    def compute_scores(self) -> None:
+        """Scores + straggler masks into the packed device buffer (one kernel on 1 GPU;
+        partials -> RCCL all_gather -> finalize on N GPUs)."""
         R, K = self.R, self.K
         st = self.stats.view(R, K)
         self.err.zero_()
-        if self.relative:
-            ops.kernel_ref(st.num, st.med, ref=self.ref, scratch=self.ref_scratch)
-        ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid,
-                   ref=self.ref if self.relative else None, hist=self.hist,
-                   partials=self.partials, err=self.err)
-        if self.world > 1:
+        ref = self.col_ref.view(torch.float32)[:K] if self.relative else None
+        missing = self.col_ref[K:2 * K] if self.relative else None
+        if self.world == 1:
+            ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
+                       ref_missing=missing, hist=self.hist, err=self.err,
+                       finalize=self._outputs())
+            return
+        ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
+                   ref_missing=missing, hist=self.hist, partials=self.partials, err=self.err)
+        if self.gloo:  # gloo collectives take host tensors
+            h = self.partials.cpu()
+            hg = torch.empty((self.world, R, 6), dtype=torch.float64)
+            torch.distributed.all_gather_into_tensor(hg, h, group=self.group)
+            self.gathered.copy_(hg)
+        else:          # RCCL over xGMI, device to device
             torch.distributed.all_gather_into_tensor(self.gathered, self.partials, group=self.group)
-            return self.gathered
-        return self.partials
+        o = self._outputs()
+        ops.finalize_scores(self.gathered, R, self.world, self.round_f32, self.thr_rel,
+                            self.thr_ind, rel=self.relative, ind=self.individual, err=self.err,
+                            out={k: o[k] for k in ("gpu_rel", "gpu_ind", "strag_rel", "strag_ind")})
 
-    def finalize(self, partials: torch.Tensor) -> BatchResult:
-        nshards = partials.shape[0] if partials.dim() == 3 else 1
-        gr, gi, sr, si = ops.finalize_scores(partials, self.R, nshards, self.round_f32,
-                                             self.thr_rel, self.thr_ind, rel=self.relative,
-                                             ind=self.individual, err=self.err)
-        if gr is not None:
-            self.h_scores[0].copy_(gr, non_blocking=True)
-            self.h_masks[0].copy_(sr, non_blocking=True)
-        if gi is not None:
-            self.h_scores[1].copy_(gi, non_blocking=True)
-            self.h_masks[1].copy_(si, non_blocking=True)
-        self.h_err.copy_(self.err, non_blocking=True)
+    def land(self) -> BatchResult:
+        """The one device-to-host copy of the packed results, then host views."""
+        self.h_out.copy_(self.out, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
-        return BatchResult(
-            self.h_scores[0].numpy().copy() if gr is not None else None,
-            self.h_scores[1].numpy().copy() if gi is not None else None,
-            self.h_masks[0].numpy().astype(bool) if gr is not None else None,
-            self.h_masks[1].numpy().astype(bool) if gi is not None else None,
-            int(self.h_err[0]),
-        )
+        R = self.R
+        h = self.h_out.numpy()
+        gr = h[0:8 * R].view(np.float64).copy() if self.relative else None
+        gi = h[8 * R:16 * R].view(np.float64).copy() if self.individual else None
+        sr = h[16 * R:17 * R].astype(bool) if self.relative else None
+        si = h[17 * R:18 * R].astype(bool) if self.individual else None
+        return BatchResult(gr, gi, sr, si, int(h[self._e:self._e + 4].view(np.int32)[0]))
 
     def report(self, ns: torch.Tensor, s_push: int) -> BatchResult:
         """One full report: samples resident in HBM -> scores + straggler sets on host."""
         self.compute_stats(ns, s_push)
-        return self.finalize(self.compute_partials())
+        self.compute_scores()
+        return self.land()

@@ -54,7 +54,8 @@ def _stream(stream):
 
 def segment_stats_strided(ns: torch.Tensor, nseg: int, seg_stride: int, seg_begin: int,
                           seg_len: int, cap: int = 0, mode: int = STATS_FAST,
-                          out: Optional[SegmentStats] = None, stream=None) -> SegmentStats:
+                          out: Optional[SegmentStats] = None, col_ref: Optional[torch.Tensor] = None,
+                          ncols: int = 0, stream=None) -> SegmentStats:
     """Stats of segments ns.flat[s*seg_stride + seg_begin : +seg_len] (uint32 ns), last
     `cap` samples retained (CircularBuffer.h:53-69).  reference: CuptiProfiler.cpp:44-74."""
     N.require_device(ns, "ns")
@@ -65,8 +66,10 @@ def segment_stats_strided(ns: torch.Tensor, nseg: int, seg_stride: int, seg_begi
     if out is None:
         out = SegmentStats.empty(nseg, ns.device)
     soa = out.soa()
+    if col_ref is not None and (col_ref.numel() < 2 * ncols or col_ref.dtype != torch.int32):
+        raise ValueError("col_ref must be an int32 tensor of >= 2*ncols elements")
     N.call("nvrx_segment_stats_strided", ns.data_ptr(), nseg, seg_stride, seg_begin, seg_len,
-           cap, mode, ctypes.byref(soa), _stream(stream))
+           cap, mode, ctypes.byref(soa), N.ptr(col_ref), ncols, _stream(stream))
     return out
 
 
@@ -110,30 +113,39 @@ def pack_min_times(med: torch.Tensor, ids: torch.Tensor, total: int,
     return out
 
 
-def scores(num, med, avg, *, col_valid=None, ref=None, ref_index=None, hist=None,
-           hist_index=None, hist_stride=0, partials=None, err=None, stream=None) -> torch.Tensor:
-    """Per-row partial sums {sum s*w, sum w, n} for rel and indiv (reporting.py:219-253)."""
+def scores(num, med, avg, *, col_valid=None, ref=None, ref_index=None, ref_missing=None,
+           hist=None, hist_index=None, hist_stride=0, partials=None, err=None,
+           finalize: Optional[dict] = None, stream=None):
+    """Per-row partial sums {sum s*w, sum w, n} for rel and indiv (reporting.py:219-253).
+    finalize = dict(gpu_rel=, gpu_ind=, strag_rel=, strag_ind=, thr_rel=, thr_ind=,
+    round_f32=) finishes the scores in the same kernel (single shard)."""
     R, K = med.shape
-    if partials is None:
+    if partials is None and finalize is None:
         partials = torch.empty((R, 6), dtype=torch.float64, device=med.device)
     f64 = med.dtype == torch.float64
     if avg.dtype != med.dtype or (hist is not None and hist.dtype != med.dtype):
         raise TypeError("med, avg and hist must share one float dtype")
-    a = N.ScoreArgs(R, K, int(f64), num.data_ptr(), med.data_ptr(), avg.data_ptr(), N.ptr(col_valid),
-                    N.ptr(ref), N.ptr(ref_index), N.ptr(hist), N.ptr(hist_index), hist_stride,
-                    partials.data_ptr(), N.ptr(err))
+    fz = finalize or {}
+    a = N.ScoreArgs(R, K, int(f64), num.data_ptr(), med.data_ptr(), avg.data_ptr(),
+                    N.ptr(col_valid), N.ptr(ref), N.ptr(ref_index), N.ptr(ref_missing),
+                    N.ptr(hist), N.ptr(hist_index), hist_stride, N.ptr(partials), N.ptr(err),
+                    int(fz.get("round_f32", False)), float(fz.get("thr_rel", 0.75)),
+                    float(fz.get("thr_ind", 0.75)), N.ptr(fz.get("gpu_rel")),
+                    N.ptr(fz.get("gpu_ind")), N.ptr(fz.get("strag_rel")), N.ptr(fz.get("strag_ind")))
     N.call("nvrx_scores", ctypes.byref(a), _stream(stream))
     return partials
 
 
 def finalize_scores(partials: torch.Tensor, R: int, nshards: int = 1, round_f32: bool = False,
                     thr_rel: float = 0.75, thr_ind: float = 0.75, rel=True, ind=True, err=None,
-                    stream=None):
+                    out: Optional[dict] = None, stream=None):
+    """Scores + straggler masks from [nshards][R][6] partials (shards summed in order)."""
     dev = partials.device
-    gr = torch.empty(R, dtype=torch.float64, device=dev) if rel else None
-    gi = torch.empty(R, dtype=torch.float64, device=dev) if ind else None
-    sr = torch.empty(R, dtype=torch.uint8, device=dev) if rel else None
-    si = torch.empty(R, dtype=torch.uint8, device=dev) if ind else None
+    o = out or {}
+    gr = o.get("gpu_rel", torch.empty(R, dtype=torch.float64, device=dev) if rel else None)
+    gi = o.get("gpu_ind", torch.empty(R, dtype=torch.float64, device=dev) if ind else None)
+    sr = o.get("strag_rel", torch.empty(R, dtype=torch.uint8, device=dev) if rel else None)
+    si = o.get("strag_ind", torch.empty(R, dtype=torch.uint8, device=dev) if ind else None)
     N.call("nvrx_finalize_scores", partials.data_ptr(), R, nshards, int(round_f32),
            float(thr_rel), float(thr_ind), N.ptr(gr), N.ptr(gi), N.ptr(sr), N.ptr(si),
            N.ptr(err), _stream(stream))

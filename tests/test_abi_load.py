@@ -41,7 +41,8 @@ def test_lib_loads_and_reports_abi():
 def test_argument_errors_raise_runtime_error_without_gpu():
     # host-side checks run before any launch: a bad mode is rejected with a message
     soa = _native.StatsSoA(1, 1, 1, 1, 1, 1)
-    rc = _native.lib().nvrx_segment_stats_strided(1, 1, 8, 0, 8, 0, 9, ctypes.byref(soa), None)
+    rc = _native.lib().nvrx_segment_stats_strided(1, 1, 8, 0, 8, 0, 9, ctypes.byref(soa), None, 0,
+                                                  None)
     assert rc == _native.NVRX_ERR_INVALID
     assert b"mode" in _native.lib().nvrx_last_error()
     with pytest.raises(RuntimeError, match="mode"):
