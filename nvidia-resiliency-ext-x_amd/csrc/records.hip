@@ -21,8 +21,13 @@
 
 namespace nvrx {
 
+// Per-stream slack for the 16-B padding of every bucket (<= 3 per slot), itself a
+// multiple of 4 elements so that every stream base stays 16-byte aligned.
+__host__ __device__ __forceinline__ int64_t stream_slack(int64_t nslots) {
+    return (3 * nslots + 4 + 3) & ~(int64_t)3;
+}
 __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t, int64_t nslots) {
-    return ((rec_off[t] + 3) & ~(int64_t)3) + t * (3 * nslots + 4);
+    return ((rec_off[t] + 3) & ~(int64_t)3) + t * stream_slack(nslots);
 }
 
 __global__ __launch_bounds__(64) void records_bucket_kernel(const nvrx_record* __restrict__ recs,
@@ -120,7 +125,7 @@ __global__ __launch_bounds__(64) void records_bucket_kernel(const nvrx_record* _
 }
 
 int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
-    return ((n + 3) & ~(int64_t)3) + nstreams * (3 * nslots + 4);
+    return ((n + 3) & ~(int64_t)3) + nstreams * stream_slack(nslots);
 }
 
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,

@@ -105,13 +105,13 @@ class MatrixReporter:
             return
         ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
                    ref_missing=missing, hist=self.hist, partials=self.partials, err=self.err)
+        flat = self.gathered.view(self.world * R, 6)
         if self.gloo:  # gloo collectives take host tensors
-            h = self.partials.cpu()
-            hg = torch.empty((self.world, R, 6), dtype=torch.float64)
-            torch.distributed.all_gather_into_tensor(hg, h, group=self.group)
-            self.gathered.copy_(hg)
+            hg = torch.empty((self.world * R, 6), dtype=torch.float64)
+            torch.distributed.all_gather_into_tensor(hg, self.partials.cpu(), group=self.group)
+            flat.copy_(hg)
         else:          # RCCL over xGMI, device to device
-            torch.distributed.all_gather_into_tensor(self.gathered, self.partials, group=self.group)
+            torch.distributed.all_gather_into_tensor(flat, self.partials, group=self.group)
         o = self._outputs()
         ops.finalize_scores(self.gathered, R, self.world, self.round_f32, self.thr_rel,
                             self.thr_ind, rel=self.relative, ind=self.individual, err=self.err,

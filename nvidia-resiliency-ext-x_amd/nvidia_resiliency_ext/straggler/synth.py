@@ -43,11 +43,12 @@ def kernel_names(K: int) -> List[str]:
 
 
 def kernel_hash(name: str) -> int:
-    """64-bit FNV-1a of the composite kernel name (the shard key of the multi-GPU path)."""
+    """Shard key of the multi-GPU path: 64-bit FNV-1a of the composite kernel name, finalised
+    with splitmix64 so that the low bits (used by % n_gpus) are well mixed."""
     h = 0xCBF29CE484222325
     for b in name.encode():
         h = ((h ^ b) * 0x100000001B3) & M64
-    return h
+    return splitmix64(h)
 
 
 def shard_kernels(names: Sequence[str], nshards: int, shard: int) -> np.ndarray:

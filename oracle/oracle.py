@@ -67,6 +67,7 @@ def lib():
         L.oracle_matrix_stats.argtypes = [P, i64, i64, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
         L.oracle_kernel_ref.argtypes = [P, P, i64, i64, P]
         L.oracle_scores.argtypes = [P, P, P, i64, i64, P, P, P, P, P]
+        L.oracle_score_partials.argtypes = [P, P, P, i64, i64, P, P, P, P]
         L.oracle_stragglers.restype = i64
         L.oracle_stragglers.argtypes = [P, i64, ctypes.c_double, P]
         _lib = L
@@ -167,6 +168,21 @@ def scores(num, med, avg, col_valid=None, ref=None, hist=None, rel=True, indiv=T
     lib().oracle_scores(_p(num), _p(med), _p(avg), R, K, _p(col_valid), _p(ref), _p(hist),
                         _p(gr), _p(gi))
     return gr, gi
+
+
+def score_partials(num, med, avg, ref, col_in_shard=None, hist=None) -> np.ndarray:
+    """[R][6] partial sums over the columns of one shard (rel: s*w, w, n; indiv: same)."""
+    num = np.ascontiguousarray(num, np.int32)
+    med = np.ascontiguousarray(med, np.float32)
+    avg = np.ascontiguousarray(avg, np.float32)
+    R, K = num.shape
+    if hist is None:
+        hist = np.full((R, K), np.inf, np.float64)
+    out = np.empty((R, 6), np.float64)
+    mask = None if col_in_shard is None else np.ascontiguousarray(col_in_shard, np.uint8)
+    lib().oracle_score_partials(_p(num), _p(med), _p(avg), R, K, _p(mask),
+                                _p(np.ascontiguousarray(ref, np.float32)), _p(hist), _p(out))
+    return out
 
 
 def stragglers(score: np.ndarray, thr: float) -> np.ndarray:

@@ -1,0 +1,176 @@
+"""GPU: the device-resident record log + ring retention (records.hip) and the profiler
+handle that replaces nvrx_cupti_module.CuptiProfiler (test_cupti_ext.py / test_cupti_manager.py
+semantics restated)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from nvidia_resiliency_ext.straggler import cupti, ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_slot_stats(durations, cap):
+    st = O.compute_stats(O.ring_linearize(O.ns_to_us(np.asarray(durations, np.uint32)), cap))
+    return (st.num_calls, np.float32(st.min), np.float32(st.max), np.float32(st.median),
+            np.float32(st.avg), np.float32(st.stddev))
+
+
+def _streams(rng, nstreams, nslots, lo, hi):
+    """push-ordered record streams {slot, ns} with per-slot counts in [lo, hi]"""
+    recs, off = [], [0]
+    for _ in range(nstreams):
+        counts = rng.integers(lo, hi + 1, size=nslots)
+        slots = np.repeat(np.arange(nslots, dtype=np.uint32), counts)
+        rng.shuffle(slots)
+        ns = rng.integers(1000, 5_000_000, size=slots.size, dtype=np.uint32)
+        recs.append(np.stack([slots, ns], axis=1))
+        off.append(off[-1] + slots.size)
+    return np.concatenate(recs), np.array(off, np.int64)
+
+
+@pytest.mark.parametrize("cap,lo,hi", [(8192, 0, 40), (7, 0, 30), (16, 10, 100), (3, 0, 5)])
+def test_records_bucket_keeps_last_cap_per_slot(cap, lo, hi):
+    rng = np.random.default_rng(cap * 7 + hi)
+    nstreams, nslots = 5, 37
+    recs, off = _streams(rng, nstreams, nslots, lo, hi)
+    d_recs = torch.from_numpy(recs.view(np.int32)).cuda()
+    seg_off, seg_len, out_ns, counts = ops.records_bucket(d_recs, torch.from_numpy(off).cuda(),
+                                                          nslots, cap)
+    seg_off, seg_len, out_ns, counts = (t.cpu().numpy() for t in (seg_off, seg_len, out_ns, counts))
+    for t in range(nstreams):
+        stream = recs[off[t]:off[t + 1]]
+        for s in range(nslots):
+            pushed = stream[stream[:, 0] == s, 1]
+            g = t * nslots + s
+            assert counts[g] == pushed.size
+            kept = pushed[-cap:] if cap > 0 else pushed
+            assert seg_len[g] == kept.size
+            assert seg_off[g] % 4 == 0  # 16-byte aligned runs
+            got = out_ns[seg_off[g]:seg_off[g] + seg_len[g]].view(np.uint32)
+            if pushed.size > cap:  # overflowed rings are written in push order
+                assert np.array_equal(got, kept)
+            else:
+                assert np.array_equal(np.sort(got), np.sort(kept))
+    # the buckets feed the segment-stats kernel directly (aligned runs)
+    st = ops.segment_stats_ragged(torch.from_numpy(out_ns).cuda(), torch.from_numpy(seg_off).cuda(),
+                                  torch.from_numpy(seg_len).cuda(), max_len=max(1, int(seg_len.max())),
+                                  cap=cap, mode=ops.STATS_EXACT, aligned16=True).cpu()
+    for t in range(nstreams):
+        stream = recs[off[t]:off[t + 1]]
+        for s in range(nslots):
+            g = t * nslots + s
+            pushed = stream[stream[:, 0] == s, 1]
+            if pushed.size == 0:
+                assert st.num[g].item() == 0
+                continue
+            r = _oracle_slot_stats(pushed, cap)
+            got = (st.num[g].item(), np.float32(st.min[g]), np.float32(st.max[g]),
+                   np.float32(st.med[g]), np.float32(st.avg[g]), np.float32(st.std[g]))
+            assert got == r, (t, s)
+
+
+@pytest.fixture
+def profiler():
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=8192)
+    yield p
+    p.close()
+
+
+def test_profiler_singleton(profiler):
+    with pytest.raises(RuntimeError):
+        cupti.KernelProfiler()
+
+
+def test_profiler_stats_bit_exact_and_name_sorted(profiler):
+    rng = np.random.default_rng(3)
+    profiler.initialize()
+    profiler.start()
+    pushed = {}
+    for name in ["zeta_kernel_blk_64_1_1_grid_8_1_1", "alpha_blk_256_1_1_grid_1_1_1", "mid_k"]:
+        d = rng.integers(1000, 900_000, size=int(rng.integers(1, 3000)), dtype=np.uint32)
+        profiler.push(name, d)
+        pushed[name] = d
+    stats = profiler.get_stats()
+    assert list(stats) == sorted(pushed)
+    for name, d in pushed.items():
+        s = stats[name]
+        r = _oracle_slot_stats(d, 8192)
+        assert (s.num_calls, np.float32(s.min), np.float32(s.max), np.float32(s.median),
+                np.float32(s.avg), np.float32(s.stddev)) == r, name
+    profiler.stop()
+    profiler.push("ignored_while_stopped", [5, 6, 7])  # activity disabled: not captured
+    assert "ignored_while_stopped" not in profiler.get_stats()
+    profiler.reset()
+    assert profiler.get_stats() == {}
+
+
+def test_profiler_ring_cap_seven():
+    # test_cupti_ext.py:107-127: statsMaxLenPerKernel=7, 21 executions -> num_calls == 7
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=7)
+    try:
+        p.initialize()
+        p.start()
+        p.push("mm_kernel", [1000 * (i + 1) for i in range(21)])
+        s = p.get_stats()["mm_kernel"]
+        assert s.num_calls == 7 and s.min == 15.0 and s.max == 21.0 and s.median == 18.0
+        # results survive stop; a later start keeps accumulating (test_cupti_ext.py:23-105)
+        p.stop()
+        p.start()
+        p.push("mm_kernel", [50_000])
+        s = p.get_stats()["mm_kernel"]
+        assert s.num_calls == 7 and s.max == 50.0 and s.min == 16.0
+    finally:
+        p.close()
+
+
+def test_profiler_compaction_keeps_retention_semantics():
+    cap = 5
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=cap)
+    try:
+        p.initialize()
+        p.start()
+        rng = np.random.default_rng(9)
+        n = (1 << 22) + 4096  # past the compaction threshold
+        slots = rng.integers(0, 3, size=n).astype(np.uint32)
+        ns = rng.integers(1000, 2_000_000, size=n, dtype=np.uint32)
+        for name in ("k0", "k1", "k2"):
+            p.register_kernel(name)
+        p.push_slots(slots, ns)
+        p.get_stats()  # flush -> compaction (log >> retained records)
+        p.push_slots(np.array([1, 1], np.uint32), np.array([7, 9], np.uint32))
+        st = p.get_stats()
+        for s, name in enumerate(("k0", "k1", "k2")):
+            d = ns[slots == s]
+            if s == 1:
+                d = np.concatenate([d, [7, 9]]).astype(np.uint32)
+            r = _oracle_slot_stats(d, cap)
+            got = st[name]
+            assert (got.num_calls, np.float32(got.min), np.float32(got.max),
+                    np.float32(got.median)) == r[:4], name
+    finally:
+        p.close()
+
+
+def test_cupti_manager_refcount():
+    # test_cupti_manager.py:23-87
+    m = cupti.CuptiManager(statsMaxLenPerKernel=64)
+    try:
+        with pytest.raises(RuntimeError):
+            m.start_profiling()  # not initialized
+        m.initialize()
+        m.start_profiling()
+        m.start_profiling()
+        m.push("k", [1000, 2000])
+        m.stop_profiling()
+        m.push("k", [3000])           # still started (refcount 1)
+        m.stop_profiling()
+        m.push("k", [4000])           # stopped: dropped
+        assert m.get_results()["k"].num_calls == 3
+        with pytest.raises(RuntimeError):
+            m.stop_profiling()
+        m.reset_results()
+        assert m.get_results() == {}
+    finally:
+        m.shutdown()
