@@ -81,6 +81,61 @@ __device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned v) {
     return v;
 }
 
+// Per-lane sums of the samples d[0..PL) held in registers.
+//   sd = sum d, exact: 64-bit add-with-carry on 32-bit halves (keeps v[] 32-bit; a zext
+//        to i64 lets the scheduler widen every sample to a register pair and spill).
+//   sq = sum (d - c)^2 about a pivot c that is one of the segment's own samples, so the
+//        variance sq/n - ((sd - n c)/n)^2 does not cancel against the mean even for
+//        tightly clustered durations with far outliers.  Squares accumulate in f32 over
+//        two chains of <= 8 terms and are folded into f64: relative error ~1e-7
+//        (tests/test_gpu_segment_stats.py bounds it against an f64 reference).
+template <int PL>
+__device__ __forceinline__ void lane_sums(const unsigned (&v)[PL], unsigned c, uint64_t& sd,
+                                          double& sq) {
+    unsigned lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+    double acc = 0.0;
+    constexpr int G = PL < 16 ? PL : 16;
+#pragma unroll
+    for (int g = 0; g < PL; g += G) {
+        float q0 = 0.0f, q1 = 0.0f;
+#pragma unroll
+        for (int i = 0; i < G; i += 2) {
+            unsigned c0, c1;
+            lo0 = __builtin_addc(lo0, v[g + i], 0u, &c0);
+            hi0 += c0;
+            lo1 = __builtin_addc(lo1, v[g + i + 1], 0u, &c1);
+            hi1 += c1;
+            const float fa = (float)(int)(v[g + i] - c), fb = (float)(int)(v[g + i + 1] - c);
+            q0 = __builtin_fmaf(fa, fa, q0);
+            q1 = __builtin_fmaf(fb, fb, q1);
+        }
+        acc += (double)q0 + (double)q1;
+    }
+    sd = ((uint64_t)hi0 << 32 | lo0) + ((uint64_t)hi1 << 32 | lo1);
+    sq = acc;
+}
+
+// Same sums with f64 squares about c = 0, for masked segments whose padding holds d = 0
+// (contributes nothing to either sum).
+template <int PL>
+__device__ __forceinline__ void lane_sums_f64(const unsigned (&v)[PL], uint64_t& sd, double& sq) {
+    unsigned lo0 = 0, hi0 = 0, lo1 = 0, hi1 = 0;
+    double q0 = 0.0, q1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < PL; i += 2) {
+        unsigned c0, c1;
+        lo0 = __builtin_addc(lo0, v[i], 0u, &c0);
+        hi0 += c0;
+        lo1 = __builtin_addc(lo1, v[i + 1], 0u, &c1);
+        hi1 += c1;
+        const double fa = (double)v[i], fb = (double)v[i + 1];
+        q0 = __builtin_fma(fa, fa, q0);
+        q1 = __builtin_fma(fb, fb, q1);
+    }
+    sd = ((uint64_t)hi0 << 32 | lo0) + ((uint64_t)hi1 << 32 | lo1);
+    sq = q0 + q1;
+}
+
 // CuptiProfiler.cpp:187 -- (end - start) / 1000.0f: integer ns -> f32 (round to
 // nearest) -> correctly-rounded IEEE divide (hipcc lowers '/' to the
 // div_scale/div_fmas/div_fixup sequence; the build never enables fast-math).

@@ -23,6 +23,8 @@
 //   samples converted to f32 us, bitonic-sorted in LDS, then AVG = sequential f32
 //   sum over the sorted samples and STD = sqrtf(sequential sum of squares / n),
 //   exactly as CuptiProfiler.cpp:63-69 -- every field bit-exact.
+#include <stdlib.h>
+
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
@@ -63,11 +65,21 @@ struct ColRef {
     uint32_t* minbits;
     uint32_t* missing;
     int64_t ncols;
+    double inv;  // 1.0 / ncols
+    // s % ncols without a 64-bit integer divide: the f64 quotient is off by at most one
+    // for s < 2^52
+    __device__ __forceinline__ int64_t col(int64_t s) const {
+        int64_t q = (int64_t)((double)s * inv);
+        int64_t r = s - q * ncols;
+        if (r < 0) r += ncols;
+        if (r >= ncols) r -= ncols;
+        return r;
+    }
     __device__ __forceinline__ void add(int64_t s, float med) const {
-        if (minbits) atomicMin(&minbits[s % ncols], __float_as_uint(med));
+        if (minbits) atomicMin(&minbits[col(s)], __float_as_uint(med));
     }
     __device__ __forceinline__ void miss(int64_t s) const {
-        if (minbits) atomicOr(&missing[s % ncols], 1u);
+        if (minbits) atomicOr(&missing[col(s)], 1u);
     }
 };
 
@@ -80,6 +92,46 @@ __device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) 
     o.med[s] = q;
     o.avg[s] = q;
     o.std[s] = q;
+}
+
+// Epilogue of the FAST kernels, lane-parallel: lanes 0-3 convert MIN, MAX, s[t0], s[t1]
+// in one ns_to_us, lanes 0/1 form avg and std in one f64 divide; lane 0 stores.
+//   sd = sum(d), sq = sum((d - c)^2) over the n samples, d = x - MIN.
+//   avg = (n MIN + sd) / (1000 n)               (numerator exact in f64)
+//   std = sqrt(n sq - (sd - n c)^2) / (1000 n)   (population std, CuptiProfiler.cpp:66-70)
+__device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, int n,
+                                           unsigned mn, unsigned mx, unsigned d0, unsigned d1,
+                                           double sd, double sq, unsigned c, const ColRef& cr) {
+    const int lane = lane_id();
+    const unsigned x = lane == 0 ? mn : lane == 1 ? mx : lane == 2 ? mn + d0 : mn + d1;
+    const float f = ns_to_us(x);
+    const float fmn = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 0));
+    const float fmx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 1));
+    const float f0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 2));
+    const float f1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 3));
+    // CuptiProfiler.cpp:58: f32 add, exact halving
+    const float med = (n & 1) ? f0 : (f0 + f1) / 2;
+    const double dn = (double)n;
+    const double se = sd - dn * (double)c;  // exact: integers < 2^53
+    double num;
+    if (lane == 0) {
+        num = __builtin_fma((double)mn, dn, sd);
+    } else {
+        const double v = __builtin_fma(sq, dn, -(se * se));
+        num = __builtin_sqrt(v > 0.0 ? v : 0.0);
+    }
+    const float r = (float)(num / (1000.0 * dn));
+    const float avg = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 0));
+    const float sdv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 1));
+    if (lane == 0) {
+        o.num[s] = n;
+        o.min[s] = fmn;
+        o.max[s] = fmx;
+        o.med[s] = med;
+        o.avg[s] = avg;
+        o.std[s] = sdv;
+        cr.add(s, med);
+    }
 }
 
 template <int PL>
@@ -148,6 +200,148 @@ struct OccV {  // the masked PL=128 variant gets the whole 256-register budget
     static constexpr int W = (!FULL && PL >= 128) ? 2 : Occ<PL>::W;
 };
 
+// cache policy of the once-read sample stream (buffer-load aux bits)
+#ifndef NVRX_LOAD_AUX
+#define NVRX_LOAD_AUX 2  // nt: measured +1.5-2% on C2/C3 over the default policy
+#endif
+
+// Reduce one segment held in registers (v: 64*PL slots, lane-interleaved in 16-B
+// vectors; element i of the wave holds sample e = (j*64 + lane)*4 + t - m0, i = 4j + t).
+// FULL: every slot is a sample (m0 = 0, n = 64*PL).  !FULL: slots outside [0, n) were
+// set to x0 (a sample) by the caller.
+template <int PL, bool FULL>
+__device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
+                                          int64_t s, unsigned* hist, const nvrx_stats_soa& out,
+                                          const ColRef& cr) {
+    constexpr int NB = Bins<PL>::NB;
+    constexpr int LOGNB = Bins<PL>::LOG;
+    constexpr int BPL = Bins<PL>::BPL;
+    const int lane = lane_id();
+    const int pad = FULL ? 0 : 64 * PL - n;  // padding elements (not samples of the segment)
+
+    // ---- pass A1: MIN / MAX ----
+    unsigned lmn = v[0], lmx = v[0];
+#pragma unroll
+    for (int i = 1; i < PL; ++i) {
+        lmn = min(lmn, v[i]);
+        lmx = max(lmx, v[i]);
+    }
+    const unsigned mn = wave_min_u32(lmn);
+    const unsigned mx = wave_max_u32(lmx);
+
+    // From here on v holds d = x - MIN (in place: one register per sample).
+    // Padding := d 0 (= MIN): contributes 0 to the sums below and occupies the lowest
+    // `pad` ranks, so the median ranks simply shift by `pad`.
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        if (FULL) {
+            v[i] -= mn;
+        } else {
+            const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
+            v[i] = (e < (unsigned)n) ? v[i] - mn : 0u;
+        }
+    }
+
+    const unsigned range = mx - mn;
+    const int bits = 32 - __clz((int)range);  // 0 when range == 0
+    int shift = bits > LOGNB ? bits - LOGNB : 0;
+
+    // ---- pass A2: exact sums + first histogram level ----
+    // pivot c: the segment's first sample, when every d - c fits an int (FULL segments
+    // spanning < 2^31 ns); otherwise c = 0 with f64 squares (padding holds d = 0)
+    const bool pivot = FULL && range < 0x80000000u;
+    const unsigned c = pivot ? x0 - mn : 0u;
+    uint64_t sdl;
+    double sql;
+    if (pivot)
+        lane_sums<PL>(v, c, sdl, sql);
+    else
+        lane_sums_f64<PL>(v, sdl, sql);
+    const double sd = wave_sum_f64((double)sdl);  // exact: integer-valued, < 2^53
+    const double sq = wave_sum_f64(sql);
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < PL; ++i) atomicAdd(&hist[v[i] >> shift], 1u);
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- median: radix select on d = x - MIN ----
+    // sorted real samples s[0..n); median = odd ? s[n/2] : (s[n/2-1] + s[n/2]) / 2
+    const unsigned t0 = (unsigned)(pad + ((n & 1) ? n / 2 : n / 2 - 1));
+    const unsigned t1 = (unsigned)(pad + n / 2);
+    unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
+    for (int level = 0;; ++level) {
+        if (level > 0) {
+#pragma unroll
+            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+            __builtin_amdgcn_wave_barrier();
+            const unsigned span = (unsigned)NB << shift;  // level > 0: fits in 32 bits
+#pragma unroll
+            for (int i = 0; i < PL; ++i) {
+                const unsigned q = v[i] - wlo;  // wraps for d < wlo
+                if (q < span) atomicAdd(&hist[q >> shift], 1u);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        unsigned b0, c0, n0, b1, c1, n1;
+        hist_locate2<PL>(hist, t0 - below, t1 - below, b0, c0, n0, b1, c1, n1);
+        if (b0 != b1) {
+            // s[t0] is the largest sample of bucket b0, s[t1] the smallest of bucket b1
+            unsigned lmax = 0, lmin = 0xFFFFFFFFu;
+            const unsigned lo0 = wlo + (b0 << shift), lo1 = wlo + (b1 << shift);
+            const unsigned width = 1u << shift;
+#pragma unroll
+            for (int i = 0; i < PL; ++i) {
+                const unsigned d = v[i];
+                if (d - lo0 < width) lmax = max(lmax, d);
+                if (d - lo1 < width) lmin = min(lmin, d);
+            }
+            d0 = wave_max_u32(lmax);
+            d1 = wave_min_u32(lmin);
+            break;
+        }
+        if (shift == 0) {
+            d0 = d1 = wlo + b0;
+            break;
+        }
+        if (n0 <= 64u) {
+            // compact the <= 64 candidates of bucket b0 into LDS (the histogram is consumed)
+            __builtin_amdgcn_wave_barrier();
+            unsigned base = 0;
+            const unsigned lo0 = wlo + (b0 << shift);
+            const unsigned width = 1u << shift;
+#pragma unroll
+            for (int i = 0; i < PL; ++i) {
+                const unsigned d = v[i];
+                const bool in = d - lo0 < width;
+                const uint64_t bm = __ballot(in);
+                if (in) hist[base + mbcnt(bm)] = d;
+                base += (unsigned)__popcll(bm);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
+            unsigned rank = 0;
+            for (int j = 0; j < (int)n0; ++j) {
+                const unsigned cj = __builtin_amdgcn_readlane(ci, j);
+                rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
+            }
+            const unsigned r0 = t0 - below - c0, r1 = t1 - below - c0;
+            const int L0 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r0)) - 1;
+            const int L1 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r1)) - 1;
+            d0 = __builtin_amdgcn_readlane(ci, L0);
+            d1 = __builtin_amdgcn_readlane(ci, L1);
+            break;
+        }
+        // descend one level into bucket b0
+        below += c0;
+        wlo += b0 << shift;
+        shift = shift > LOGNB ? shift - LOGNB : 0;
+    }
+
+    emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
+}
+
 // FULL: the host guarantees every segment holds exactly 64*PL samples starting on a
 // 16-byte boundary, so no lane needs masking.  !FULL: per-element masks (branch-free).
 template <int PL, bool FULL, class Segs>
@@ -155,8 +349,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OccV<PL, FU
 void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
     constexpr int NV = PL / 4;
     constexpr int NB = Bins<PL>::NB;
-    constexpr int LOGNB = Bins<PL>::LOG;
-    constexpr int BPL = Bins<PL>::BPL;
     __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
 
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -192,14 +384,12 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     unsigned v[PL];
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 16, j * 1024, 0);
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 16, j * 1024, NVRX_LOAD_AUX);
         v[4 * j + 0] = q.x;
         v[4 * j + 1] = q.y;
         v[4 * j + 2] = q.z;
         v[4 * j + 3] = q.w;
     }
-    const int pad = FULL ? 0 : 64 * PL - n;  // padding elements (not samples of the segment)
-    // element i of the wave holds sample e = (j*64 + lane)*4 + t - m0 (i = 4j + t)
     if (!FULL) {
 #pragma unroll
         for (int i = 0; i < PL; ++i) {
@@ -207,146 +397,7 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
             v[i] = (e < (unsigned)n) ? v[i] : x0;  // x0 is a sample: neutral for min/max
         }
     }
-
-    // ---- pass A1: MIN / MAX ----
-    unsigned lmn = v[0], lmx = v[0];
-#pragma unroll
-    for (int i = 1; i < PL; ++i) {
-        lmn = min(lmn, v[i]);
-        lmx = max(lmx, v[i]);
-    }
-    const unsigned mn = wave_min_u32(lmn);
-    const unsigned mx = wave_max_u32(lmx);
-
-    // From here on v holds d = x - MIN (in place: one register per sample).
-    // Padding := d 0 (= MIN): contributes 0 to the sums below and occupies the lowest
-    // `pad` ranks, so the median ranks simply shift by `pad`.
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-        if (FULL) {
-            v[i] -= mn;
-        } else {
-            const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
-            v[i] = (e < (unsigned)n) ? v[i] - mn : 0u;
-        }
-    }
-
-    const unsigned range = mx - mn;
-    const int bits = 32 - __clz((int)range);  // 0 when range == 0
-    int shift = bits > LOGNB ? bits - LOGNB : 0;
-
-    // ---- pass A2: exact sums + first histogram level ----
-#pragma unroll
-    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
-    __builtin_amdgcn_wave_barrier();
-    // two independent f64 chains each; the d sums are integers < 2^53: exact in f64
-    double sd0 = 0.0, sd1 = 0.0, sq0 = 0.0, sq1 = 0.0;
-#pragma unroll
-    for (int i = 0; i < PL; i += 2) {
-        const unsigned da = v[i], db = v[i + 1];
-        const double fa = (double)da, fb = (double)db;
-        sd0 += fa;
-        sd1 += fb;
-        sq0 = __builtin_fma(fa, fa, sq0);
-        sq1 = __builtin_fma(fb, fb, sq1);
-        atomicAdd(&hist[da >> shift], 1u);
-        atomicAdd(&hist[db >> shift], 1u);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const double sd = wave_sum_f64(sd0 + sd1);  // exact: integer-valued, < 2^53
-    const double sq = wave_sum_f64(sq0 + sq1);
-
-    // ---- median: radix select on d = x - MIN ----
-    // sorted real samples s[0..n); median = odd ? s[n/2] : (s[n/2-1] + s[n/2]) / 2
-    const unsigned t0 = (unsigned)(pad + ((n & 1) ? n / 2 : n / 2 - 1));
-    const unsigned t1 = (unsigned)(pad + n / 2);
-    unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
-    for (int level = 0;; ++level) {
-        if (level > 0) {
-#pragma unroll
-            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const unsigned d = v[i];
-                const unsigned q = d - wlo;
-                if (d >= wlo && (q >> shift) < (unsigned)NB) atomicAdd(&hist[q >> shift], 1u);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        unsigned b0, c0, n0, b1, c1, n1;
-        hist_locate2<PL>(hist, t0 - below, t1 - below, b0, c0, n0, b1, c1, n1);
-        if (b0 != b1) {
-            // s[t0] is the largest sample of bucket b0, s[t1] the smallest of bucket b1
-            unsigned lmax = 0, lmin = 0xFFFFFFFFu;
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const unsigned d = v[i];
-                const unsigned q = d - wlo;
-                const bool inw = d >= wlo;
-                const unsigned bk = q >> shift;
-                if (inw && bk == b0) lmax = max(lmax, d);
-                if (inw && bk == b1) lmin = min(lmin, d);
-            }
-            d0 = wave_max_u32(lmax);
-            d1 = wave_min_u32(lmin);
-            break;
-        }
-        if (shift == 0) {
-            d0 = d1 = wlo + b0;
-            break;
-        }
-        if (n0 <= 64u) {
-            // compact the <= 64 candidates of bucket b0 into LDS (the histogram is consumed)
-            __builtin_amdgcn_wave_barrier();
-            unsigned base = 0;
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const unsigned d = v[i];
-                const bool in = (d >= wlo) && (((d - wlo) >> shift) == b0);
-                const uint64_t bm = __ballot(in);
-                if (in) hist[base + mbcnt(bm)] = d;
-                base += (unsigned)__popcll(bm);
-            }
-            __builtin_amdgcn_wave_barrier();
-            const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
-            unsigned rank = 0;
-            for (int j = 0; j < (int)n0; ++j) {
-                const unsigned cj = __builtin_amdgcn_readlane(ci, j);
-                rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
-            }
-            const unsigned r0 = t0 - below - c0, r1 = t1 - below - c0;
-            const int L0 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r0)) - 1;
-            const int L1 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r1)) - 1;
-            d0 = __builtin_amdgcn_readlane(ci, L0);
-            d1 = __builtin_amdgcn_readlane(ci, L1);
-            break;
-        }
-        // descend one level into bucket b0
-        below += c0;
-        wlo += b0 << shift;
-        shift = shift > LOGNB ? shift - LOGNB : 0;
-    }
-
-    if (lane == 0) {
-        out.num[s] = n;
-        out.min[s] = ns_to_us(mn);
-        out.max[s] = ns_to_us(mx);
-        const float f0 = ns_to_us(mn + d0);
-        float med = f0;
-        if (!(n & 1)) {
-            const float f1 = ns_to_us(mn + d1);
-            med = (f0 + f1) / 2;  // f32 add, exact halving (CuptiProfiler.cpp:58)
-        }
-        out.med[s] = med;
-        cr.add(s, med);
-        const double dn = (double)n;
-        const double mean_d = sd / dn;
-        out.avg[s] = (float)(((double)mn + mean_d) / 1000.0);
-        double var = sq / dn - mean_d * mean_d;
-        var = var > 0.0 ? var : 0.0;
-        out.std[s] = (float)(__builtin_sqrt(var) / 1000.0);
-    }
+    fast_body<PL, FULL>(v, n, m0, x0, s, hist, out, cr);
 }
 
 // ---------------------------------------------------------------------------
@@ -475,9 +526,9 @@ hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_s
                                  int64_t seg_begin, int64_t seg_len, int64_t cap, int mode,
                                  const nvrx_stats_soa& out, uint32_t* col_ref, int64_t ncols,
                                  hipStream_t st) {
-    ColRef cr{nullptr, nullptr, 1};
+    ColRef cr{nullptr, nullptr, 1, 1.0};
     if (col_ref && ncols > 0) {
-        cr = ColRef{col_ref, col_ref + ncols, ncols};
+        cr = ColRef{col_ref, col_ref + ncols, ncols, 1.0 / (double)ncols};
         hipError_t e = hipMemsetD32Async((hipDeviceptr_t)col_ref, 0x7F800000, (size_t)ncols, st);
         if (e == hipSuccess)
             e = hipMemsetD32Async((hipDeviceptr_t)(col_ref + ncols), 0, (size_t)ncols, st);
@@ -491,6 +542,17 @@ hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_s
                          ((((uintptr_t)(ns + seg_begin + (seg_len - keep))) & 15) == 0);
     const int64_t need = aligned ? keep : keep + 3;
     if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
+    // NVRX_ROWS_MAX (env, default 0 = off): longest retained segment sent to the rows
+    // kernel (4 segments per wave); measured slower than one wave per segment at C3
+    static const int64_t rows_max = [] {
+        const char* e = getenv("NVRX_ROWS_MAX");
+        return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    if (need <= rows_max && need <= 16 * 64 && nseg >= 4) {  // short segments: 4 per wave
+        hipError_t e = segment_stats_rows(ns, nseg, seg_stride, seg_begin, seg_len, cap, out,
+                                          cr.minbits, cr.missing, cr.ncols, st);
+        if (e != hipErrorNotSupported) return e;
+    }
     // every strided segment has the same length and (aligned) phase
     return launch_fast(segs, nseg, need, aligned ? keep : -1, out, cr, st);
 }
@@ -503,7 +565,7 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
     if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
     const int64_t need = aligned16 ? keep : keep + 3;
-    const ColRef cr{nullptr, nullptr, 1};
+    const ColRef cr{nullptr, nullptr, 1, 1.0};
     if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
     return launch_fast(segs, nseg, need, -1, out, cr, st);  // lengths vary: masked variant
 }

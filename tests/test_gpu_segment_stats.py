@@ -119,6 +119,8 @@ def _edge_segments(n):
                         np.array([1, 4_000_000_000, 7][:min(n, 3)], np.uint32)]),
         (rng.integers(0, 2**20, size=n) * 4096 + 5).astype(np.uint32),  # sparse keys
         np.zeros(n, np.uint32),                                          # 0-ns durations
+        # tight cluster + one low outlier: variance far below mean^2 (cancellation-prone)
+        np.where(np.arange(n) == n - 1, 10, 100_000 + rng.integers(0, 20, size=n)).astype(np.uint32),
     ]
     return segs
 
@@ -185,3 +187,45 @@ def test_shape_errors_raise():
         ops.segment_stats_strided(ns, 2, 60, 0, 60)
     with pytest.raises(RuntimeError):
         ops.segment_stats_strided(ns, 1, 100, 0, 100, cap=0, mode=7)
+
+
+# ---- the 4-segments-per-wave kernel (segment_rows.hip): strided, stride % 4 == 0, <= 1024 kept
+@pytest.mark.parametrize("length", [1, 2, 3, 5, 16, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257,
+                                    511, 512, 513, 1000, 1021, 1024])
+@pytest.mark.parametrize("nseg", [4, 5, 7, 33])
+def test_rows_kernel_parity(length, nseg):
+    rng = np.random.default_rng(length * 100 + nseg)
+    for begin in (0, 1, 2, 3):
+        stride = (length + begin + 3) // 4 * 4 + 4 * int(rng.integers(0, 3))
+        host = rng.integers(1000, 3_000_000, size=nseg * stride, dtype=np.uint32)
+        ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+        st = ops.segment_stats_strided(ns, nseg, stride, begin, length, cap=0, mode=ops.STATS_FAST)
+        ref = _oracle_segments(host, nseg, stride, begin, length, 0)
+        _check(st, ref, avg_std=_exact_avg_std(host, nseg, stride, begin, length, 0))
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 64, 100, 1024])
+def test_rows_kernel_edge_distributions(n):
+    segs = _edge_segments(n)
+    stride = (n + 3) // 4 * 4
+    host = np.zeros(len(segs) * stride, np.uint32)
+    for i, sgm in enumerate(segs):
+        host[i * stride:i * stride + n] = sgm
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    st = ops.segment_stats_strided(ns, len(segs), stride, 0, n, cap=0, mode=ops.STATS_FAST)
+    _check(st, _oracle_segments(host, len(segs), stride, 0, n, 0))
+
+
+def test_rows_kernel_config3_shape_with_colref():
+    # configs[2] shape scaled down: S=1024 per (rank, kernel), and a pushed-1500 / cap-1024 ring
+    for S, cap in ((1024, 8192), (1500, 1024)):
+        R, K = 9, 24
+        ns = synth.synth_matrix(R, K, S, device=DEV)
+        col = torch.empty(2 * K, dtype=torch.int32, device=DEV)
+        st = ops.segment_stats_strided(ns.view(-1), R * K, S, 0, S, cap=cap, col_ref=col, ncols=K)
+        host = ns.cpu().numpy().view(np.uint32).reshape(-1)
+        ref = _oracle_segments(host, R * K, S, 0, S, cap)
+        _check(st, ref, avg_std=_exact_avg_std(host, R * K, S, 0, S, cap))
+        want = O.kernel_ref(ref["num"].reshape(R, K), ref["med"].reshape(R, K))
+        got = col.cpu().numpy()
+        assert np.array_equal(got[:K].view(np.float32), want) and not got[K:].any()
