@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NVRX_ABI_VERSION 1
+#define NVRX_ABI_VERSION 2
 
 #define NVRX_OK 0
 #define NVRX_ERR_INVALID -1   /* bad argument / shape */
@@ -120,10 +120,13 @@ int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_str
 /* Segment s = ns[seg_off[s] : seg_off[s] + seg_len[s]] (device arrays; seg_len NULL:
  * seg_off has nseg+1 entries and segment s ends at seg_off[s+1]); max_len bounds every
  * segment length (host-known); aligned16 != 0 promises every retained run starts on a
- * 16-byte boundary. */
+ * 16-byte boundary.  col_ref / ncols: as for the strided call (segment s is row s / ncols,
+ * column s % ncols).  Segments of <= 64 retained samples are bit-exact in every field in
+ * both modes (one lane per segment, the reference's sequential f32 sums). */
 int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
                               int64_t nseg, int64_t max_len, int64_t cap, int32_t mode,
-                              int32_t aligned16, const nvrx_stats_soa* out, void* stream);
+                              int32_t aligned16, const nvrx_stats_soa* out, uint32_t* col_ref,
+                              int64_t ncols, void* stream);
 
 /* ---------------------------------------------------------------- scoring */
 /* ref[k] = min over r of med[r][k] if num[r][k] > 0 for every r, else NaN.

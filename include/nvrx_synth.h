@@ -18,6 +18,11 @@ extern "C" {
 int nvrx_synth_matrix(uint32_t* out, int64_t R, int64_t K_local, int64_t K_global,
                       const int64_t* kmap, int64_t s_push, uint64_t seed, uint64_t seed2,
                       const uint8_t* straggler, void* stream);
+/* Record streams (configs[3]): out[r*N + j] = {slot[j], ns}, ns the occ[j]-th sample of
+ * kernel slot[j] on rank r under the hash above with S_push = s_push, K = K. */
+int nvrx_synth_records(uint32_t* out, int64_t R, int64_t N, const uint32_t* slot,
+                       const uint32_t* occ, int64_t K, int64_t s_push, uint64_t seed,
+                       uint64_t seed2, const uint8_t* straggler, void* stream);
 #ifdef __cplusplus
 }
 #endif

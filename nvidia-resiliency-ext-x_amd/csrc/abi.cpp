@@ -83,7 +83,8 @@ int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_str
 
 int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
                               int64_t nseg, int64_t max_len, int64_t cap, int32_t mode,
-                              int32_t aligned16, const nvrx_stats_soa* out, void* stream) {
+                              int32_t aligned16, const nvrx_stats_soa* out, uint32_t* col_ref,
+                              int64_t ncols, void* stream) {
     NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
                    "nvrx_segment_stats_ragged: null output array");
     NVRX_CHECK_ARG(nseg >= 0 && max_len >= 0, "nvrx_segment_stats_ragged: negative size");
@@ -94,8 +95,10 @@ int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const 
     NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT,
                    "nvrx_segment_stats_ragged: retained segment longer than NVRX_MAX_SEGMENT");
     NVRX_CHECK_ARG(nseg < (int64_t)1 << 31, "nvrx_segment_stats_ragged: too many segments");
+    NVRX_CHECK_ARG(!col_ref || (ncols > 0 && nseg % ncols == 0),
+                   "nvrx_segment_stats_ragged: col_ref needs ncols > 0 dividing nseg");
     return hip_status(nvrx::segment_stats_ragged(ns, seg_off, seg_len, nseg, max_len, cap, mode,
-                                                 aligned16 != 0, *out, S(stream)),
+                                                 aligned16 != 0, *out, col_ref, ncols, S(stream)),
                       "nvrx_segment_stats_ragged");
 }
 
@@ -502,7 +505,7 @@ int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, u
     const int64_t cap = p->cfg.stats_max_len_per_kernel;
     hipError_t e = nvrx::segment_stats_ragged(w.ns, w.seg_off, w.seg_len, nslots,
                                               std::min<int64_t>(cap, p->log_n), cap, p->cfg.mode,
-                                              true, soa, p->stream);
+                                              true, soa, nullptr, 0, p->stream);
     if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: segment_stats");
     std::vector<int32_t> hnum(nslots);
     std::vector<float> hmn(nslots), hmx(nslots), hmed(nslots), havg(nslots), hsd(nslots);

@@ -11,13 +11,10 @@ hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_s
                                  int64_t seg_begin, int64_t seg_len, int64_t cap, int mode,
                                  const nvrx_stats_soa& out, uint32_t* col_ref, int64_t ncols,
                                  hipStream_t st);
-hipError_t segment_stats_rows(const uint32_t* ns, int64_t nseg, int64_t stride, int64_t begin,
-                              int64_t len, int64_t cap, const nvrx_stats_soa& out,
-                              uint32_t* minbits, uint32_t* missing, int64_t ncols,
-                              hipStream_t st);
 hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
                                 int64_t nseg, int64_t max_len, int64_t cap, int mode,
-                                bool aligned16, const nvrx_stats_soa& out, hipStream_t st);
+                                bool aligned16, const nvrx_stats_soa& out, uint32_t* col_ref,
+                                int64_t ncols, hipStream_t st);
 
 hipError_t kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
                       uint32_t* scratch, hipStream_t st);

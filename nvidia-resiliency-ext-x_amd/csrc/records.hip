@@ -8,14 +8,16 @@
 // slot are kept.  computeStats sorts, so order inside a bucket does not change any
 // statistic; buckets are still written in push order whenever a slot overflowed.
 //
-// One 64-lane wave owns one stream; per-slot counters live in LDS:
-//   pass 1: LDS histogram of slots;
+// One workgroup of RB_WAVES waves owns one stream; per-slot counters live in LDS:
+//   pass 1: LDS histogram of slots (every wave a contiguous quarter of the stream,
+//           16-byte loads = two records per lane);
 //   scan  : keep_s = min(count_s, cap), bucket starts padded to 16 B (aligned loads
 //           in segment_stats), written to seg_off / seg_len / counts;
-//   pass 2: scatter.  No slot overflowed -> LDS atomic slot cursors (order-free);
-//           else a stable pass: 64 records per step, same-slot lanes grouped with
-//           ballot (leader = lowest lane), occurrence index = cursor + mbcnt(group),
-//           record kept iff occurrence >= count - keep.
+//   pass 2: scatter.  Records of slots that did not overflow take LDS atomic cursors
+//           (order inside such a bucket is free: computeStats sorts); records of
+//           overflowed slots are placed by wave 0 alone, in push order: 64 records per
+//           step, same-slot lanes grouped with ballot (leader = lowest lane), occurrence
+//           index = cursor + mbcnt(group), kept iff occurrence >= count - keep.
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
@@ -30,78 +32,103 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
     return ((rec_off[t] + 3) & ~(int64_t)3) + t * stream_slack(nslots);
 }
 
-__global__ __launch_bounds__(64) void records_bucket_kernel(const nvrx_record* __restrict__ recs,
-                                                            const int64_t* __restrict__ rec_off,
-                                                            int64_t nslots, int64_t cap,
-                                                            int force_stable, int64_t* seg_off,
-                                                            int32_t* seg_len, uint32_t* out_ns,
-                                                            int32_t* counts) {
+constexpr int RB_WAVES = 4;
+constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
+
+// records [lo, hi) of a stream in 16-byte pairs where the base allows it; f(rec) per record
+template <class F>
+__device__ __forceinline__ void for_records(const nvrx_record* rs, int64_t lo, int64_t hi, int lane,
+                                            bool pairs, F&& f) {
+    if (pairs) {  // lo, hi even; rs 16-B aligned
+        const uint4* q = (const uint4*)(rs + lo);
+        const int64_t np = (hi - lo) >> 1;
+        for (int64_t i = lane; i < np; i += 64) {
+            const uint4 w = q[i];
+            f(nvrx_record{w.x, w.y});
+            f(nvrx_record{w.z, w.w});
+        }
+    } else {
+        for (int64_t i = lo + lane; i < hi; i += 64) f(rs[i]);
+    }
+}
+
+__global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
+    const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
+    int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
+    int32_t* counts) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
-    uint32_t* start = lds + 2 * nslots; // [nslots] bucket start (relative to stream base)
+    uint32_t* start = lds + 2 * nslots; // [nslots] bucket start (relative to stream base) | RB_OVF
+    __shared__ uint32_t any_ovf;
     const int64_t t = blockIdx.x;
     const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
     const int64_t r0 = rec_off[t], r1 = rec_off[t + 1];
     const nvrx_record* rs = recs + r0;
     const int64_t n = r1 - r0;
     const int64_t base = stream_base(rec_off, t, nslots);
+    const bool pairs = (((uintptr_t)rs) & 15) == 0;
+    // wave w's chunk: [lo, hi), even boundaries
+    const int64_t per = ((n + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
+    const int64_t lo = min(n, per * wave), hi = min(n, lo + per);
+    const bool wpairs = pairs && ((hi - lo) % 2 == 0);
 
-    for (int64_t s = lane; s < nslots; s += 64) {
+    for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
         cnt[s] = 0u;
         cur[s] = 0u;
     }
+    if (threadIdx.x == 0) any_ovf = force_stable ? 1u : 0u;
     __syncthreads();
-    for (int64_t i = lane; i < n; i += 64) {
-        const uint32_t s = rs[i].slot;
-        if (s < (uint32_t)nslots) atomicAdd(&cnt[s], 1u);
-    }
+    for_records(rs, lo, hi, lane, wpairs, [&](const nvrx_record& r) {
+        if (r.slot < (uint32_t)nslots) atomicAdd(&cnt[r.slot], 1u);
+    });
     __syncthreads();
 
-    // exclusive scan of padded keeps over slots, 64 at a time with a running carry
-    uint32_t carry = 0;
-    bool overflow = false;
-    for (int64_t c = 0; c < nslots; c += 64) {
-        const int64_t s = c + lane;
-        uint32_t keep = 0, total = 0;
-        if (s < nslots) {
-            total = cnt[s];
-            keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
-            overflow |= (keep != total);
+    // exclusive scan of padded keeps over slots (wave 0), 64 at a time with a carry
+    if (wave == 0) {
+        uint32_t carry = 0;
+        bool overflow = false;
+        for (int64_t c = 0; c < nslots; c += 64) {
+            const int64_t s = c + lane;
+            uint32_t keep = 0, total = 0;
+            if (s < nslots) {
+                total = cnt[s];
+                keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+            }
+            const bool ovf = keep != total;
+            overflow |= ovf;
+            const uint32_t padded = (keep + 3u) & ~3u;
+            const uint32_t incl = wave_incl_scan_u32(padded);
+            const uint32_t st = carry + incl - padded;
+            if (s < nslots) {
+                start[s] = st | (ovf || force_stable ? RB_OVF : 0u);
+                const int64_t g = t * nslots + s;
+                seg_off[g] = base + st;
+                seg_len[g] = (int32_t)keep;
+                counts[g] = (int32_t)total;
+            }
+            carry += __builtin_amdgcn_readlane(incl, 63);
         }
-        const uint32_t padded = (keep + 3u) & ~3u;
-        const uint32_t incl = wave_incl_scan_u32(padded);
-        const uint32_t st = carry + incl - padded;
-        if (s < nslots) {
-            start[s] = st;
-            const int64_t g = t * nslots + s;
-            seg_off[g] = base + st;
-            seg_len[g] = (int32_t)keep;
-            counts[g] = (int32_t)total;
-        }
-        carry += __builtin_amdgcn_readlane(incl, 63);
+        if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
     }
-    overflow = (__ballot(overflow) != 0) || force_stable;
     __syncthreads();
     uint32_t* out = out_ns + base;
 
-    if (!overflow) {
-        for (int64_t i = lane; i < n; i += 64) {
-            const nvrx_record rec = rs[i];
-            if (rec.slot < (uint32_t)nslots) {
-                const uint32_t pos = atomicAdd(&cur[rec.slot], 1u);
-                out[start[rec.slot] + pos] = rec.ns;
-            }
+    // records of slots that kept everything: any order
+    for_records(rs, lo, hi, lane, wpairs, [&](const nvrx_record& r) {
+        if (r.slot < (uint32_t)nslots) {
+            const uint32_t st = start[r.slot];
+            if (!(st & RB_OVF)) out[st + atomicAdd(&cur[r.slot], 1u)] = r.ns;
         }
-        return;
-    }
-    // stable pass: occurrence index of each record within its slot, push order
+    });
+    if (!any_ovf || wave != 0) return;
+    // overflowed slots: wave 0 walks the whole stream in push order
     for (int64_t b = 0; b < n; b += 64) {
         const int64_t i = b + lane;
-        const bool valid = i < n;
         nvrx_record rec = {0xFFFFFFFFu, 0u};
-        if (valid) rec = rs[i];
-        const bool ok = valid && rec.slot < (uint32_t)nslots;
+        if (i < n) rec = rs[i];
+        const bool ok = rec.slot < (uint32_t)nslots && (start[rec.slot] & RB_OVF);
         uint64_t pending = __ballot(ok);
         uint32_t occ = 0;
         while (pending) {
@@ -109,7 +136,7 @@ __global__ __launch_bounds__(64) void records_bucket_kernel(const nvrx_record* _
             const uint32_t ls = __builtin_amdgcn_readlane(rec.slot, leader);
             const uint64_t grp = __ballot(ok && rec.slot == ls) & pending;
             const uint32_t c0 = cur[ls];
-            if (rec.slot == ls && ok) occ = c0 + mbcnt(grp);
+            if (ok && rec.slot == ls) occ = c0 + mbcnt(grp);
             __builtin_amdgcn_wave_barrier();
             if (lane == leader) cur[ls] = c0 + (uint32_t)__popcll(grp);
             __builtin_amdgcn_wave_barrier();
@@ -119,7 +146,7 @@ __global__ __launch_bounds__(64) void records_bucket_kernel(const nvrx_record* _
             const uint32_t total = cnt[rec.slot];
             const uint32_t keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
             const uint32_t drop = total - keep;
-            if (occ >= drop) out[start[rec.slot] + (occ - drop)] = rec.ns;
+            if (occ >= drop) out[(start[rec.slot] & ~RB_OVF) + (occ - drop)] = rec.ns;
         }
     }
 }
@@ -142,7 +169,7 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(records_bucket_kernel, dim3((unsigned)nstreams), dim3(64), lds, st, recs,
+    hipLaunchKernelGGL(records_bucket_kernel, dim3((unsigned)nstreams), dim3(64 * RB_WAVES), lds, st, recs,
                        rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts);
     return hipGetLastError();
 }

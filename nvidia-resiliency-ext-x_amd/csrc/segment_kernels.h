@@ -1,0 +1,529 @@
+// segment_kernels.h -- device code shared by the segment-statistics launchers
+// (segment_stats.hip: strided / one-shot; segment_ragged.hip: length classes).
+// See segment_stats.hip for the algorithm.
+#pragma once
+#include "nvrx_common.h"
+#include "nvrx_internal.h"
+
+namespace nvrx {
+
+// ---------------------------------------------------------------------------
+// Segment addressing
+// ---------------------------------------------------------------------------
+struct StridedSegs {  // segment s = base[s*stride + begin : + len], last `cap` kept
+    const uint32_t* base;
+    int64_t stride, begin, len, cap;
+    __device__ __forceinline__ void get(int64_t s, const uint32_t*& p, int& n) const {
+        int64_t keep = (cap > 0 && len > cap) ? cap : len;
+        p = base + s * stride + begin + (len - keep);
+        n = (int)keep;
+    }
+};
+struct RaggedSegs {  // segment s = base[off[s] : off[s] + len[s]] (len NULL: off[s+1]), last `cap` kept
+    const uint32_t* base;
+    const int64_t* off;
+    const int32_t* lens;
+    int64_t cap;
+    __device__ __forceinline__ void get(int64_t s, const uint32_t*& p, int& n) const {
+        const int64_t b = off[s];
+        const int64_t e = lens ? b + lens[s] : off[s + 1];
+        const int64_t len = e - b;
+        int64_t keep = (cap > 0 && len > cap) ? cap : len;
+        p = base + (e - keep);
+        n = (int)keep;
+    }
+};
+
+// Optional fused per-column reference (segment s = row s / ncols, column s % ncols):
+// minbits[c] = atomicMin of the float bits of MED (non-negative floats order like their
+// bit patterns), missing[c] |= 1 for an empty segment -- _all_reduce_times'
+// MIN-over-ranks with the -1 => NaN rule (reporting.py:255-296), done in the epilogue.
+struct ColRef {
+    uint32_t* minbits;
+    uint32_t* missing;
+    int64_t ncols;
+    double inv;  // 1.0 / ncols
+    // s % ncols without a 64-bit integer divide: the f64 quotient is off by at most one
+    // for s < 2^52
+    __device__ __forceinline__ int64_t col(int64_t s) const {
+        int64_t q = (int64_t)((double)s * inv);
+        int64_t r = s - q * ncols;
+        if (r < 0) r += ncols;
+        if (r >= ncols) r -= ncols;
+        return r;
+    }
+    __device__ __forceinline__ void add(int64_t s, float med) const {
+        if (minbits) atomicMin(&minbits[col(s)], __float_as_uint(med));
+    }
+    __device__ __forceinline__ void miss(int64_t s) const {
+        if (minbits) atomicOr(&missing[col(s)], 1u);
+    }
+};
+
+__device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) {
+    // KernelStats() default: num_calls 0, every float NaN (CuptiProfiler.h:39-45)
+    const float q = __builtin_nanf("");
+    o.num[s] = 0;
+    o.min[s] = q;
+    o.max[s] = q;
+    o.med[s] = q;
+    o.avg[s] = q;
+    o.std[s] = q;
+}
+
+// Epilogue of the FAST kernels, lane-parallel: lanes 0-3 convert MIN, MAX, s[t0], s[t1]
+// in one ns_to_us, lanes 0/1 form avg and std in one f64 divide; lane 0 stores.
+//   sd = sum(d), sq = sum((d - c)^2) over the n samples, d = x - MIN.
+//   avg = (n MIN + sd) / (1000 n)               (numerator exact in f64)
+//   std = sqrt(n sq - (sd - n c)^2) / (1000 n)   (population std, CuptiProfiler.cpp:66-70)
+__device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, int n,
+                                           unsigned mn, unsigned mx, unsigned d0, unsigned d1,
+                                           double sd, double sq, unsigned c, const ColRef& cr) {
+    const int lane = lane_id();
+    const unsigned x = lane == 0 ? mn : lane == 1 ? mx : lane == 2 ? mn + d0 : mn + d1;
+    const float f = ns_to_us(x);
+    const float fmn = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 0));
+    const float fmx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 1));
+    const float f0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 2));
+    const float f1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 3));
+    // CuptiProfiler.cpp:58: f32 add, exact halving
+    const float med = (n & 1) ? f0 : (f0 + f1) / 2;
+    const double dn = (double)n;
+    const double se = sd - dn * (double)c;  // exact: integers < 2^53
+    double num;
+    if (lane == 0) {
+        num = __builtin_fma((double)mn, dn, sd);
+    } else {
+        const double v = __builtin_fma(sq, dn, -(se * se));
+        num = __builtin_sqrt(v > 0.0 ? v : 0.0);
+    }
+    const float r = (float)(num / (1000.0 * dn));
+    const float avg = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 0));
+    const float sdv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 1));
+    if (lane == 0) {
+        o.num[s] = n;
+        o.min[s] = fmn;
+        o.max[s] = fmx;
+        o.med[s] = med;
+        o.avg[s] = avg;
+        o.std[s] = sdv;
+        cr.add(s, med);
+    }
+}
+
+template <int PL>
+struct Bins {
+    static constexpr int NB = (8 * PL < 64) ? 64 : (8 * PL > 512) ? 512 : 8 * PL;  // bins per wave
+    static constexpr int BPL = NB / 64;                     // bins per lane
+    static constexpr int LOG = (NB == 64) ? 6 : (NB == 128) ? 7 : (NB == 256) ? 8 : (NB == 512) ? 9 : 10;
+    static_assert((1 << LOG) == NB, "NB must be a power of two <= 1024");
+};
+
+// Locate the buckets holding relative ranks ta <= tb in the wave's histogram (one read
+// of the bins).  For each: bucket index, elements in lower buckets, count of the bucket.
+template <int PL>
+__device__ __forceinline__ void hist_locate2(const unsigned* hist, unsigned ta, unsigned tb,
+                                             unsigned& ba, unsigned& bfa, unsigned& ca,
+                                             unsigned& bb, unsigned& bfb, unsigned& cb) {
+    constexpr int BPL = Bins<PL>::BPL;
+    const int lane = lane_id();
+    unsigned h[BPL];
+    unsigned local = 0;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        h[j] = hist[lane * BPL + j];
+        local += h[j];
+    }
+    const unsigned incl = wave_incl_scan_u32(local);
+    const unsigned excl = incl - local;
+    // first lane whose range reaches the target (< 64 since target < total)
+    const int La = __popcll(__ballot(incl <= ta));
+    const int Lb = __popcll(__ballot(incl <= tb));
+    unsigned run = excl, sa = 0, pa = 0, na = 0, sb = 0, pb = 0, nb = 0;
+    bool fa = false, fb = false;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        const unsigned nxt = run + h[j];
+        if (!fa && nxt > ta) {
+            fa = true;
+            sa = (unsigned)(lane * BPL + j);
+            pa = run;
+            na = h[j];
+        }
+        if (!fb && nxt > tb) {
+            fb = true;
+            sb = (unsigned)(lane * BPL + j);
+            pb = run;
+            nb = h[j];
+        }
+        run = nxt;
+    }
+    ba = __builtin_amdgcn_readlane(sa, La);
+    bfa = __builtin_amdgcn_readlane(pa, La);
+    ca = __builtin_amdgcn_readlane(na, La);
+    bb = __builtin_amdgcn_readlane(sb, Lb);
+    bfb = __builtin_amdgcn_readlane(pb, Lb);
+    cb = __builtin_amdgcn_readlane(nb, Lb);
+}
+
+// Occupancy target per PL: the samples take PL VGPRs; ask the register allocator for
+// enough waves per SIMD that HBM latency is covered by other waves' segments.
+template <int PL>
+struct Occ {
+    static constexpr int W = PL >= 128 ? 3 : PL >= 64 ? 4 : PL >= 32 ? 6 : 8;
+};
+template <int PL, bool FULL>
+struct OccV {  // the masked PL=128 variant gets the whole 256-register budget
+    static constexpr int W = (!FULL && PL >= 128) ? 2 : Occ<PL>::W;
+};
+
+// cache policy of the once-read sample stream (buffer-load aux bits)
+#ifndef NVRX_LOAD_AUX
+#define NVRX_LOAD_AUX 2  // nt: measured +1.5-2% on C2/C3 over the default policy
+#endif
+
+// Reduce one segment held in registers (v: 64*PL slots, lane-interleaved in 16-B
+// vectors; element i of the wave holds sample e = (j*64 + lane)*4 + t - m0, i = 4j + t).
+// FULL: every slot is a sample (m0 = 0, n = 64*PL).  !FULL: slots outside [0, n) were
+// set to x0 (a sample) by the caller.
+template <int PL, bool FULL>
+__device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
+                                          int64_t s, unsigned* hist, const nvrx_stats_soa& out,
+                                          const ColRef& cr) {
+    constexpr int NB = Bins<PL>::NB;
+    constexpr int LOGNB = Bins<PL>::LOG;
+    constexpr int BPL = Bins<PL>::BPL;
+    const int lane = lane_id();
+    const int pad = FULL ? 0 : 64 * PL - n;  // padding elements (not samples of the segment)
+
+    // ---- pass A1: MIN / MAX ----
+    unsigned lmn = v[0], lmx = v[0];
+#pragma unroll
+    for (int i = 1; i < PL; ++i) {
+        lmn = min(lmn, v[i]);
+        lmx = max(lmx, v[i]);
+    }
+    const unsigned mn = wave_min_u32(lmn);
+    const unsigned mx = wave_max_u32(lmx);
+
+    // From here on v holds d = x - MIN (in place: one register per sample).
+    // Padding := d 0 (= MIN): contributes 0 to the sums below and occupies the lowest
+    // `pad` ranks, so the median ranks simply shift by `pad`.
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+        if (FULL) {
+            v[i] -= mn;
+        } else {
+            const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
+            v[i] = (e < (unsigned)n) ? v[i] - mn : 0u;
+        }
+    }
+
+    const unsigned range = mx - mn;
+    const int bits = 32 - __clz((int)range);  // 0 when range == 0
+    int shift = bits > LOGNB ? bits - LOGNB : 0;
+
+    // ---- pass A2: exact sums + first histogram level ----
+    // pivot c: the segment's first sample, when every d - c fits an int (FULL segments
+    // spanning < 2^31 ns); otherwise c = 0 with f64 squares (padding holds d = 0)
+    const bool pivot = FULL && range < 0x80000000u;
+    const unsigned c = pivot ? x0 - mn : 0u;
+    uint64_t sdl;
+    double sql;
+    if (pivot)
+        lane_sums<PL>(v, c, sdl, sql);
+    else
+        lane_sums_f64<PL>(v, sdl, sql);
+    const double sd = wave_sum_f64((double)sdl);  // exact: integer-valued, < 2^53
+    const double sq = wave_sum_f64(sql);
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < PL; ++i) atomicAdd(&hist[v[i] >> shift], 1u);
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- median: radix select on d = x - MIN ----
+    // sorted real samples s[0..n); median = odd ? s[n/2] : (s[n/2-1] + s[n/2]) / 2
+    const unsigned t0 = (unsigned)(pad + ((n & 1) ? n / 2 : n / 2 - 1));
+    const unsigned t1 = (unsigned)(pad + n / 2);
+    unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
+    for (int level = 0;; ++level) {
+        if (level > 0) {
+#pragma unroll
+            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+            __builtin_amdgcn_wave_barrier();
+            const unsigned span = (unsigned)NB << shift;  // level > 0: fits in 32 bits
+#pragma unroll
+            for (int i = 0; i < PL; ++i) {
+                const unsigned q = v[i] - wlo;  // wraps for d < wlo
+                if (q < span) atomicAdd(&hist[q >> shift], 1u);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        unsigned b0, c0, n0, b1, c1, n1;
+        hist_locate2<PL>(hist, t0 - below, t1 - below, b0, c0, n0, b1, c1, n1);
+        if (b0 != b1) {
+            // s[t0] is the largest sample of bucket b0, s[t1] the smallest of bucket b1
+            unsigned lmax = 0, lmin = 0xFFFFFFFFu;
+            const unsigned lo0 = wlo + (b0 << shift), lo1 = wlo + (b1 << shift);
+            const unsigned width = 1u << shift;
+#pragma unroll
+            for (int i = 0; i < PL; ++i) {
+                const unsigned d = v[i];
+                if (d - lo0 < width) lmax = max(lmax, d);
+                if (d - lo1 < width) lmin = min(lmin, d);
+            }
+            d0 = wave_max_u32(lmax);
+            d1 = wave_min_u32(lmin);
+            break;
+        }
+        if (shift == 0) {
+            d0 = d1 = wlo + b0;
+            break;
+        }
+        if (n0 <= 64u) {
+            // compact the <= 64 candidates of bucket b0 into LDS (the histogram is consumed)
+            __builtin_amdgcn_wave_barrier();
+            unsigned base = 0;
+            const unsigned lo0 = wlo + (b0 << shift);
+            const unsigned width = 1u << shift;
+#pragma unroll
+            for (int i = 0; i < PL; ++i) {
+                const unsigned d = v[i];
+                const bool in = d - lo0 < width;
+                const uint64_t bm = __ballot(in);
+                if (in) hist[base + mbcnt(bm)] = d;
+                base += (unsigned)__popcll(bm);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
+            unsigned rank = 0;
+            for (int j = 0; j < (int)n0; ++j) {
+                const unsigned cj = __builtin_amdgcn_readlane(ci, j);
+                rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
+            }
+            const unsigned r0 = t0 - below - c0, r1 = t1 - below - c0;
+            const int L0 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r0)) - 1;
+            const int L1 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r1)) - 1;
+            d0 = __builtin_amdgcn_readlane(ci, L0);
+            d1 = __builtin_amdgcn_readlane(ci, L1);
+            break;
+        }
+        // descend one level into bucket b0
+        below += c0;
+        wlo += b0 << shift;
+        shift = shift > LOGNB ? shift - LOGNB : 0;
+    }
+
+    emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
+}
+
+// HBM -> VGPR: the segment p[0:n) into v (64*PL slots, see fast_body), 16-byte buffer
+// loads from the 16-B aligned base below p.  m0 = p's offset in that 16-B vector (in
+// samples); x0 = p[0].  !FULL: slots outside the segment are set to x0.
+template <int PL, bool FULL>
+__device__ __forceinline__ void load_segment(const uint32_t* p, int n, unsigned (&v)[PL], int& m0,
+                                             unsigned& x0) {
+    constexpr int NV = PL / 4;
+    const int lane = lane_id();
+    // The descriptor is built from wave-uniform (readfirstlane'd) inputs so the loads
+    // issue back to back (no waterfall); lanes past the segment fall outside the
+    // descriptor's range (the hardware returns 0) and are masked below.
+    const uintptr_t pa = (uintptr_t)p & ~(uintptr_t)15;
+    m0 = (int)(((uintptr_t)p & 15) >> 2);
+    const int nvec = (n + m0 + 3) >> 2;
+    const unsigned pa_lo = __builtin_amdgcn_readfirstlane((unsigned)pa);
+    const unsigned pa_hi = __builtin_amdgcn_readfirstlane((unsigned)(pa >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(nvec * 16);
+    void* const pbase = (void*)(((uint64_t)pa_hi << 32) | pa_lo);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(pbase, 0, nbytes, 0x00020000);
+    x0 = p[0];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 16, j * 1024, NVRX_LOAD_AUX);
+        v[4 * j + 0] = q.x;
+        v[4 * j + 1] = q.y;
+        v[4 * j + 2] = q.z;
+        v[4 * j + 3] = q.w;
+    }
+    if (!FULL) {
+#pragma unroll
+        for (int i = 0; i < PL; ++i) {
+            const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
+            v[i] = (e < (unsigned)n) ? v[i] : x0;  // x0 is a sample: neutral for min/max
+        }
+    }
+}
+
+// FULL: the host guarantees every segment holds exactly 64*PL samples starting on a
+// 16-byte boundary, so no lane needs masking.  !FULL: per-element masks (branch-free).
+template <int PL, bool FULL, class Segs>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OccV<PL, FULL>::W)))
+void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
+    constexpr int NB = Bins<PL>::NB;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
+
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id();
+    const int64_t s = (int64_t)blockIdx.x * 4 + wave;
+    if (s >= nseg) return;  // wave-uniform; the kernel has no workgroup barrier
+    unsigned* hist = lds_hist + wave * NB;
+
+    const uint32_t* p;
+    int n;
+    segs.get(s, p, n);
+    if (n <= 0) {
+        if (lane == 0) {
+            write_empty(out, s);
+            cr.miss(s);
+        }
+        return;
+    }
+
+    unsigned v[PL];
+    int m0;
+    unsigned x0;
+    load_segment<PL, FULL>(p, n, v, m0, x0);
+    fast_body<PL, FULL>(v, n, m0, x0, s, hist, out, cr);
+}
+
+// ---------------------------------------------------------------------------
+// EXACT mode: one 256-thread workgroup per segment, bitonic sort in LDS.
+// ---------------------------------------------------------------------------
+// Block-wide body: the segment p[0:n), n >= 1, into sbuf[NMAX] (LDS), sorted, then the
+// reference's statistics statement by statement.  Every thread of the block calls it.
+template <int NMAX>
+__device__ __forceinline__ void exact_body(const uint32_t* p, int n, int64_t s, float* sbuf,
+                                           const nvrx_stats_soa& out, const ColRef& cr) {
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = threadIdx.x; i < np2; i += blockDim.x)
+        sbuf[i] = (i < n) ? ns_to_us(p[i]) : __builtin_inff();
+    __syncthreads();
+    // bitonic sort, ascending (+inf padding sorts last)
+    for (int k = 2; k <= np2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < np2; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const float a = sbuf[i], b = sbuf[ixj];
+                    const bool up = (i & k) == 0;
+                    if (up ? (a > b) : (a < b)) {
+                        sbuf[i] = b;
+                        sbuf[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        // CuptiProfiler.cpp:53-71, statement by statement
+        const float mnv = sbuf[0], mxv = sbuf[n - 1];
+        float med;
+        if (n % 2 == 0)
+            med = (sbuf[n / 2 - 1] + sbuf[n / 2]) / 2;
+        else
+            med = sbuf[n / 2];
+        float acc = 0.0f;
+        for (int i = 0; i < n; ++i) acc = acc + sbuf[i];
+        const float avg = acc / (float)n;
+        float sqs = 0.0f;
+        for (int i = 0; i < n; ++i) {
+            const float t = sbuf[i] - avg;
+            sqs = sqs + t * t;
+        }
+        // sqrtf, correctly rounded: f64 sqrt then one rounding to f32 is exact for sqrt
+        const float sd = (float)__builtin_sqrt((double)(sqs / (float)n));
+        out.num[s] = n;
+        out.min[s] = mnv;
+        out.max[s] = mxv;
+        out.med[s] = med;
+        cr.add(s, med);
+        out.avg[s] = avg;
+        out.std[s] = sd;
+    }
+    __syncthreads();  // sbuf is reused by the block's next segment
+}
+
+template <int NMAX, class Segs>
+__global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t nseg,
+                                                              nvrx_stats_soa out, ColRef cr) {
+    __shared__ __attribute__((aligned(16))) float sbuf[NMAX];
+    const int64_t s = blockIdx.x;
+    if (s >= nseg) return;
+    const uint32_t* p;
+    int n;
+    segs.get(s, p, n);
+    if (n <= 0) {
+        if (threadIdx.x == 0) {
+            write_empty(out, s);
+            cr.miss(s);
+        }
+        return;
+    }
+    exact_body<NMAX>(p, n, s, sbuf, out, cr);
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers shared by segment_stats.hip and segment_ragged.hip
+// ---------------------------------------------------------------------------
+// col_ref: [min med bits | missing] per column, initialised to (+inf, 0) on `st`
+static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream_t st, ColRef& cr) {
+    cr = ColRef{nullptr, nullptr, 1, 1.0};
+    if (!col_ref || ncols <= 0) return hipSuccess;
+    cr = ColRef{col_ref, col_ref + ncols, ncols, 1.0 / (double)ncols};
+    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)col_ref, 0x7F800000, (size_t)ncols, st);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(col_ref + ncols), 0, (size_t)ncols, st);
+    return e;
+}
+
+template <int PL, class Segs>
+static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
+                      const ColRef& cr, hipStream_t st) {
+    const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
+    if (full)
+        hipLaunchKernelGGL((seg_stats_fast_kernel<PL, true, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    else
+        hipLaunchKernelGGL((seg_stats_fast_kernel<PL, false, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+}
+
+// need = samples + alignment slack a wave must hold; picks the smallest PL.  `full`
+// (every segment exactly 64*PL samples, 16-B aligned) selects the unmasked variant.
+template <class Segs>
+static hipError_t launch_fast(const Segs& segs, int64_t nseg, int64_t need, int64_t exact_len,
+                              const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+    if (need <= 64 * 4)
+        launch_pl<4>(segs, nseg, exact_len == 64 * 4, out, cr, st);
+    else if (need <= 64 * 8)
+        launch_pl<8>(segs, nseg, exact_len == 64 * 8, out, cr, st);
+    else if (need <= 64 * 16)
+        launch_pl<16>(segs, nseg, exact_len == 64 * 16, out, cr, st);
+    else if (need <= 64 * 32)
+        launch_pl<32>(segs, nseg, exact_len == 64 * 32, out, cr, st);
+    else if (need <= 64 * 64)
+        launch_pl<64>(segs, nseg, exact_len == 64 * 64, out, cr, st);
+    else if (need <= 64 * 128)
+        launch_pl<128>(segs, nseg, exact_len == 64 * 128, out, cr, st);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+template <class Segs>
+static hipError_t launch_exact(const Segs& segs, int64_t nseg, int64_t max_len,
+                               const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+    const dim3 grid((unsigned)nseg), block(256);
+    if (max_len <= 1024)
+        hipLaunchKernelGGL((seg_stats_exact_kernel<1024, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    else if (max_len <= 8192)
+        hipLaunchKernelGGL((seg_stats_exact_kernel<8192, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    else if (max_len <= NVRX_MAX_SEGMENT)
+        hipLaunchKernelGGL((seg_stats_exact_kernel<NVRX_MAX_SEGMENT, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace nvrx

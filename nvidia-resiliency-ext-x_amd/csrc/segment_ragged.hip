@@ -1,0 +1,411 @@
+// segment_ragged.hip -- statistics of ragged segments (gfx950): length classes.
+//
+// Ragged inputs (the per-(rank, kernel) buckets of record streams, the profiler's
+// per-kernel rings) mix a few long segments with very many short ones: under a Zipf
+// kernel-frequency law most kernels fire a handful of times per report interval
+// (SURVEY.md 8(d), C4).  One wave per segment sized for the longest one would spend
+// 64*PL lanes-slots on a 3-sample segment, so segments are first sorted into length
+// classes and each class runs the kernel shaped for it:
+//
+//   n == 0            classifier writes the empty KernelStats (num 0, NaN) itself
+//   n <= 8 / 32 / 64  one LANE per segment: the samples in registers, a bitonic
+//                     sorting network, then CuptiProfiler.cpp:53-71 statement by
+//                     statement (sequential f32 sums) -- every field bit-exact
+//   n <= 64*PL        one WAVE per segment (fast_body, segment_kernels.h), PL 4..128
+//   longer / EXACT    one WORKGROUP per segment (exact_body)
+//
+// Classification is three small launches over the segment lengths (count per block,
+// scan, scatter) into one id list ordered by class; every class kernel is persistent
+// (grid = CUs x occupancy) and reads its [start, count) from device memory, so the
+// host never waits for the class sizes.
+#include <algorithm>
+#include <mutex>
+
+#include "segment_kernels.h"
+
+namespace nvrx {
+
+namespace {
+
+enum : int {
+    C_T8 = 0, C_T32, C_T64,                   // lane classes
+    C_W4, C_W8, C_W16, C_W32, C_W64, C_W128,  // wave classes (PL)
+    C_X,                                      // workgroup (EXACT kernel)
+    NCLASS
+};
+constexpr int CLS_THREADS = 1024;
+constexpr int CLS_MAX_BLOCKS = 1024;
+
+// need = retained samples + misalignment slack a wave would have to hold
+__device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
+    if (n <= 8) return C_T8;
+    if (n <= 32) return C_T32;
+    if (n <= 64) return C_T64;
+    if (exact) return C_X;
+    const int need = aligned16 ? n : n + 3;
+    if (need <= 64 * 4) return C_W4;
+    if (need <= 64 * 8) return C_W8;
+    if (need <= 64 * 16) return C_W16;
+    if (need <= 64 * 32) return C_W32;
+    if (need <= 64 * 64) return C_W64;
+    if (need <= 64 * 128) return C_W128;
+    return C_X;
+}
+
+// Wave-aggregated class counting: one LDS atomic per distinct class present in the
+// wave (leader = lowest lane); returns this lane's rank among same-class lanes plus the
+// class's previous count.  cls < 0: lane does not take part.
+__device__ __forceinline__ uint32_t wave_class_add(uint32_t* lcnt, int cls) {
+    uint64_t pending = __ballot(cls >= 0);
+    uint32_t mine = 0;
+    while (pending) {
+        const int leader = __builtin_ffsll(pending) - 1;
+        const int c = __builtin_amdgcn_readlane(cls, leader);
+        const uint64_t grp = __ballot(cls == c) & pending;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(&lcnt[c], (uint32_t)__popcll(grp));
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (cls == c) mine = base + mbcnt(grp);
+        pending &= ~grp;
+    }
+    return mine;
+}
+
+// pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
+__global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
+    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, uint32_t* bcnt,
+    nvrx_stats_soa out, ColRef cr) {
+    __shared__ uint32_t lcnt[NCLASS];
+    if (threadIdx.x < NCLASS) lcnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * chunk;
+    const int64_t hi = min(nseg, lo + chunk);
+    for (int64_t b = lo; b < hi; b += CLS_THREADS) {
+        const int64_t s = b + threadIdx.x;
+        int cls = -1;
+        if (s < hi) {
+            const uint32_t* p;
+            int n;
+            segs.get(s, p, n);
+            if (n <= 0) {
+                write_empty(out, s);
+                cr.miss(s);
+            } else {
+                cls = seg_class(n, aligned16 != 0, exact != 0);
+            }
+        }
+        wave_class_add(lcnt, cls);
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLASS) bcnt[(int64_t)blockIdx.x * NCLASS + threadIdx.x] = lcnt[threadIdx.x];
+}
+
+// pass 2 (one block): boff[b][c] = start of class c + blocks before b; cls[c] = {start, count}
+__global__ __launch_bounds__(CLS_MAX_BLOCKS) void classify_scan_kernel(uint32_t* bcnt, int nblocks,
+                                                                       uint32_t* cls) {
+    __shared__ uint32_t wsum[CLS_MAX_BLOCKS / 64];
+    const int b = threadIdx.x;
+    const int w = b >> 6;
+    uint32_t start = 0;
+    for (int c = 0; c < NCLASS; ++c) {
+        const uint32_t v = b < nblocks ? bcnt[(int64_t)b * NCLASS + c] : 0u;
+        const uint32_t incl = wave_incl_scan_u32(v);
+        if (lane_id() == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int j = 0; j < CLS_MAX_BLOCKS / 64; ++j) {
+            before += j < w ? wsum[j] : 0u;
+            all += wsum[j];
+        }
+        if (b < nblocks) bcnt[(int64_t)b * NCLASS + c] = start + before + incl - v;
+        if (b == 0) {
+            cls[2 * c] = start;
+            cls[2 * c + 1] = all;
+        }
+        start += all;
+        __syncthreads();
+    }
+}
+
+// pass 3: scatter segment ids into the class-ordered list
+__global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
+    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, const uint32_t* boff,
+    uint32_t* list) {
+    __shared__ uint32_t lcnt[NCLASS];
+    __shared__ uint32_t lbase[NCLASS];
+    if (threadIdx.x < NCLASS) {
+        lcnt[threadIdx.x] = 0u;
+        lbase[threadIdx.x] = boff[(int64_t)blockIdx.x * NCLASS + threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * chunk;
+    const int64_t hi = min(nseg, lo + chunk);
+    for (int64_t b = lo; b < hi; b += CLS_THREADS) {
+        const int64_t s = b + threadIdx.x;
+        int cls = -1;
+        if (s < hi) {
+            const uint32_t* p;
+            int n;
+            segs.get(s, p, n);
+            if (n > 0) cls = seg_class(n, aligned16 != 0, exact != 0);
+        }
+        const uint32_t r = wave_class_add(lcnt, cls);
+        if (cls >= 0) list[lbase[cls] + r] = (uint32_t)s;
+    }
+}
+
+// ---------------------------------------------------------------- lane classes
+// Ascending bitonic sorting network over N registers (N a power of two): compile-time
+// compare-exchanges, i.e. v_min/v_max pairs -- no LDS, no branches.
+template <int N>
+__device__ __forceinline__ void sort_net(unsigned (&v)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned a = v[i], b = v[l];
+                    const bool up = (i & k) == 0;
+                    v[i] = up ? min(a, b) : max(a, b);
+                    v[l] = up ? max(a, b) : min(a, b);
+                }
+            }
+        }
+    }
+}
+
+template <int N>
+struct LaneOcc {
+    static constexpr int W = N >= 64 ? 4 : N >= 32 ? 6 : 8;
+};
+
+// One lane per segment of 1..N samples.  u32 -> f32 us is monotone, so sorting the
+// integer ns sorts the floats computeStats sorts; then CuptiProfiler.cpp:53-71.
+template <int N>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LaneOcc<N>::W)))
+void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
+                           int aligned16, nvrx_stats_soa out, ColRef cr) {
+    const uint32_t start = cls[0], cnt = cls[1];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) {
+        const int64_t s = list[start + i];
+        const uint32_t* p;
+        int n;
+        segs.get(s, p, n);  // 1 <= n <= N
+        unsigned v[N];
+        if (aligned16) {
+            const u32x4* q = (const u32x4*)p;
+#pragma unroll
+            for (int j = 0; j < N / 4; ++j) {
+                u32x4 w = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+                if (4 * j < n) w = q[j];
+                v[4 * j + 0] = w.x;
+                v[4 * j + 1] = w.y;
+                v[4 * j + 2] = w.z;
+                v[4 * j + 3] = w.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) v[j] = j < n ? p[j] : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) v[j] = j < n ? v[j] : 0xFFFFFFFFu;  // sentinels sort last
+        sort_net<N>(v);
+        const int i0 = (n & 1) ? n / 2 : n / 2 - 1, i1 = n / 2;
+        float fmin = 0.0f, fmax = 0.0f, f0 = 0.0f, f1 = 0.0f, acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const float f = ns_to_us(v[j]);
+            v[j] = __float_as_uint(f);
+            if (j == 0) fmin = f;
+            if (j == n - 1) fmax = f;
+            if (j == i0) f0 = f;
+            if (j == i1) f1 = f;
+            acc = j < n ? acc + f : acc;  // accumulate(sorted, 0.0f): sequential f32
+        }
+        const float med = (n & 1) ? f0 : (f0 + f1) / 2;
+        const float avg = acc / (float)n;
+        float sq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const float t = __uint_as_float(v[j]) - avg;
+            sq = j < n ? sq + t * t : sq;
+        }
+        out.num[s] = n;
+        out.min[s] = fmin;
+        out.max[s] = fmax;
+        out.med[s] = med;
+        out.avg[s] = avg;
+        out.std[s] = (float)__builtin_sqrt((double)(sq / (float)n));  // sqrtf, correctly rounded
+        cr.add(s, med);
+    }
+}
+
+// ---------------------------------------------------------------- wave / workgroup classes
+template <int PL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OccV<PL, false>::W)))
+void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
+                           nvrx_stats_soa out, ColRef cr) {
+    constexpr int NB = Bins<PL>::NB;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    unsigned* hist = lds_hist + wave * NB;
+    const uint32_t start = cls[0], cnt = cls[1];
+    for (uint32_t i = blockIdx.x * 4u + wave; i < cnt; i += gridDim.x * 4u) {
+        const int64_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)list[start + i]);
+        const uint32_t* p;
+        int n;
+        segs.get(s, p, n);
+        unsigned v[PL];
+        int m0;
+        unsigned x0;
+        load_segment<PL, false>(p, n, v, m0, x0);
+        fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+    }
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void seg_stats_exact_list_kernel(RaggedSegs segs,
+                                                                   const uint32_t* list,
+                                                                   const uint32_t* cls,
+                                                                   nvrx_stats_soa out, ColRef cr) {
+    __shared__ __attribute__((aligned(16))) float sbuf[NMAX];
+    const uint32_t start = cls[0], cnt = cls[1];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const int64_t s = list[start + i];
+        const uint32_t* p;
+        int n;
+        segs.get(s, p, n);
+        exact_body<NMAX>(p, n, s, sbuf, out, cr);
+    }
+}
+
+int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+// Stream-ordered scratch from the device's default pool; the pool keeps freed blocks
+// (release threshold raised once) so steady-state reports do not return to the driver.
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+    static std::once_flag once[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        std::call_once(once[dev], [dev] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t thr = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+        });
+    }
+    return hipMallocAsync(p, bytes, st);
+}
+
+template <int N>
+void launch_lane(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls, bool aligned16,
+                 const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+    const unsigned blocks = (unsigned)(cu_count() * 2 * LaneOcc<N>::W);
+    hipLaunchKernelGGL((seg_stats_lane_kernel<N>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
+                       aligned16 ? 1 : 0, out, cr);
+}
+
+template <int PL>
+void launch_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                 const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+    const unsigned blocks = (unsigned)(cu_count() * OccV<PL, false>::W);
+    hipLaunchKernelGGL((seg_stats_list_kernel<PL>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
+                       out, cr);
+}
+
+hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                             int64_t max_len, const nvrx_stats_soa& out, const ColRef& cr,
+                             hipStream_t st) {
+    const unsigned cus = (unsigned)cu_count();
+    if (max_len <= 1024)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<1024>), dim3(cus * 8), dim3(256), 0, st, segs,
+                           list, cls, out, cr);
+    else if (max_len <= 8192)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<8192>), dim3(cus * 4), dim3(256), 0, st, segs,
+                           list, cls, out, cr);
+    else if (max_len <= NVRX_MAX_SEGMENT)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<NVRX_MAX_SEGMENT>), dim3(cus), dim3(256), 0,
+                           st, segs, list, cls, out, cr);
+    else
+        return hipErrorInvalidValue;
+    return hipSuccess;
+}
+
+}  // namespace
+
+// Below this many segments the one-shot launch (one wave per segment, PL sized for
+// max_len) is cheaper than classifying.
+constexpr int64_t RAGGED_CLASSIFY_MIN = 4096;
+
+hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
+                                int64_t nseg, int64_t max_len, int64_t cap, int mode,
+                                bool aligned16, const nvrx_stats_soa& out, uint32_t* col_ref,
+                                int64_t ncols, hipStream_t st) {
+    ColRef cr;
+    if (hipError_t e = make_colref(col_ref, ncols, st, cr); e != hipSuccess) return e;
+    if (nseg <= 0) return hipSuccess;
+    RaggedSegs segs{ns, seg_off, seg_len, cap};
+    const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
+    if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
+    const int64_t need = aligned16 ? keep : keep + 3;
+    const bool exact = mode == NVRX_STATS_EXACT;
+    if (nseg < RAGGED_CLASSIFY_MIN) {
+        if (exact || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
+        return launch_fast(segs, nseg, need, -1, out, cr, st);  // lengths vary: masked variant
+    }
+    if (nseg >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+
+    const int64_t nblocks = std::min<int64_t>(CLS_MAX_BLOCKS, (nseg + CLS_THREADS - 1) / CLS_THREADS);
+    const int64_t chunk = (nseg + nblocks - 1) / nblocks;
+    // scratch: list [nseg] | bcnt [nblocks][NCLASS] | cls [NCLASS][2]
+    const size_t bytes = (size_t)(nseg + nblocks * NCLASS + 2 * NCLASS) * sizeof(uint32_t);
+    void* ws = nullptr;
+    if (hipError_t e = scratch_alloc(&ws, bytes, st); e != hipSuccess) return e;
+    uint32_t* list = (uint32_t*)ws;
+    uint32_t* bcnt = list + nseg;
+    uint32_t* cls = bcnt + nblocks * NCLASS;
+
+    hipLaunchKernelGGL(classify_count_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st, segs,
+                       nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, out, cr);
+    hipLaunchKernelGGL(classify_scan_kernel, dim3(1), dim3(CLS_MAX_BLOCKS), 0, st, bcnt, (int)nblocks,
+                       cls);
+    hipLaunchKernelGGL(classify_scatter_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st,
+                       segs, nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, list);
+    // class kernels; classes that max_len rules out are not launched
+    const uint32_t* c = cls;
+    launch_lane<8>(segs, list, c + 2 * C_T8, aligned16, out, cr, st);
+    if (keep > 8) launch_lane<32>(segs, list, c + 2 * C_T32, aligned16, out, cr, st);
+    if (keep > 32) launch_lane<64>(segs, list, c + 2 * C_T64, aligned16, out, cr, st);
+    if (!exact) {
+        if (keep > 64) launch_list<4>(segs, list, c + 2 * C_W4, out, cr, st);
+        if (need > 64 * 4) launch_list<8>(segs, list, c + 2 * C_W8, out, cr, st);
+        if (need > 64 * 8) launch_list<16>(segs, list, c + 2 * C_W16, out, cr, st);
+        if (need > 64 * 16) launch_list<32>(segs, list, c + 2 * C_W32, out, cr, st);
+        if (need > 64 * 32) launch_list<64>(segs, list, c + 2 * C_W64, out, cr, st);
+        if (need > 64 * 64) launch_list<128>(segs, list, c + 2 * C_W128, out, cr, st);
+    }
+    if (exact ? keep > 64 : need > 64 * 128) {
+        if (hipError_t e = launch_exact_list(segs, list, c + 2 * C_X, keep, out, cr, st); e != hipSuccess)
+            return e;
+    }
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    return hipFreeAsync(ws, st);
+}
+
+}  // namespace nvrx

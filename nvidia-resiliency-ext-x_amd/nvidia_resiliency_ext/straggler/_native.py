@@ -13,6 +13,7 @@ import threading
 from typing import Optional
 
 LIB_NAME = "libnvrx_hip.so"
+ABI_VERSION = 2  # include/nvrx_straggler.h NVRX_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 NVRX_OK = 0
@@ -69,7 +70,7 @@ SIGNATURES = {
     "nvrx_segment_stats_strided": (ctypes.c_int, [P, i64, i64, i64, i64, i64, i32,
                                                   ctypes.POINTER(StatsSoA), P, i64, P]),
     "nvrx_segment_stats_ragged": (ctypes.c_int, [P, P, P, i64, i64, i64, i32, i32,
-                                                 ctypes.POINTER(StatsSoA), P]),
+                                                 ctypes.POINTER(StatsSoA), P, i64, P]),
     "nvrx_kernel_ref": (ctypes.c_int, [P, P, i64, i64, P, P, P]),
     "nvrx_pack_min_times": (ctypes.c_int, [P, P, i64, P, i64, P]),
     "nvrx_scores": (ctypes.c_int, [ctypes.POINTER(ScoreArgs), P]),
@@ -123,7 +124,7 @@ def lib() -> ctypes.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.nvrx_abi_version() != 1:
+        if L.nvrx_abi_version() != ABI_VERSION:
             raise NativeLibraryError("libnvrx_hip.so ABI version mismatch")
         _lib = L
         return _lib

@@ -2,7 +2,9 @@
 
 ``MatrixReporter`` runs the whole report for R ranks x K kernels in one pass over a
 uint32 ns matrix ``[R][K][S_push]`` (the last ``cap`` samples of every (rank, kernel)
-retained, as the reference's per-kernel rings keep them):
+retained, as the reference's per-kernel rings keep them), or over R push-ordered record
+streams ``{slot, ns}`` (``compute_stats_records``: bucket by slot keeping the last ``cap``
+of each, then length-classed segment statistics -- configs[3]):
 
   segment_stats (HIP) -> per-kernel reference = min over ranks (HIP)
   -> per-rank weighted relative / individual partial sums (HIP)
@@ -81,6 +83,32 @@ class MatrixReporter:
                                          cap=self.cap, mode=self.mode, out=self.stats,
                                          col_ref=self.col_ref if self.relative else None,
                                          ncols=self.K)
+
+    def compute_stats_records(self, recs: torch.Tensor, rec_off: torch.Tensor) -> ops.SegmentStats:
+        """recs [n, 2] int32 {slot, ns} of R streams (rec_off [R+1] int64, device): the
+        reference's ring pushes (CuptiProfiler.cpp:168-203) + getStats, for every rank."""
+        n = recs.shape[0]
+        need = ops.records_bucket_capacity(n, self.R, self.K)
+        b = getattr(self, "_bucket", None)
+        if b is None or b[2].numel() < need:
+            d = self.device
+            b = (torch.empty(self.R * self.K, dtype=torch.int64, device=d),
+                 torch.empty(self.R * self.K, dtype=torch.int32, device=d),
+                 torch.empty(max(need, 1), dtype=torch.int32, device=d),
+                 torch.empty(self.R * self.K, dtype=torch.int32, device=d))
+            self._bucket = b
+        seg_off, seg_len, out_ns, _ = ops.records_bucket(recs, rec_off, self.K, self.cap, out=b)
+        max_len = min(self.cap, n) if self.cap > 0 else n
+        return ops.segment_stats_ragged(out_ns, seg_off, seg_len, max_len=max(max_len, 1), cap=0,
+                                        mode=self.mode, aligned16=True, out=self.stats,
+                                        col_ref=self.col_ref if self.relative else None,
+                                        ncols=self.K)
+
+    def report_records(self, recs: torch.Tensor, rec_off: torch.Tensor) -> BatchResult:
+        """One full report from record streams resident in HBM."""
+        self.compute_stats_records(recs, rec_off)
+        self.compute_scores()
+        return self.land()
 
     def _outputs(self):
         v = self.views

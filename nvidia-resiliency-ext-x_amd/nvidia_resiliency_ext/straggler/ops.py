@@ -75,7 +75,10 @@ def segment_stats_strided(ns: torch.Tensor, nseg: int, seg_stride: int, seg_begi
 
 def segment_stats_ragged(ns: torch.Tensor, seg_off: torch.Tensor, seg_len: Optional[torch.Tensor],
                          max_len: int, cap: int = 0, mode: int = STATS_FAST, aligned16: bool = False,
-                         out: Optional[SegmentStats] = None, stream=None) -> SegmentStats:
+                         out: Optional[SegmentStats] = None, col_ref: Optional[torch.Tensor] = None,
+                         ncols: int = 0, stream=None) -> SegmentStats:
+    """Stats of ragged segments; segments of <= 64 retained samples are bit-exact in every
+    field.  col_ref ([2*ncols] int32): fused per-column reference, as for the strided call."""
     N.require_device(ns, "ns")
     N.require_device(seg_off, "seg_off")
     nseg = seg_off.numel() - (0 if seg_len is not None else 1)
@@ -86,7 +89,7 @@ def segment_stats_ragged(ns: torch.Tensor, seg_off: torch.Tensor, seg_len: Optio
     soa = out.soa()
     N.call("nvrx_segment_stats_ragged", ns.data_ptr(), seg_off.data_ptr(),
            N.ptr(seg_len), nseg, max_len, cap, mode, int(aligned16), ctypes.byref(soa),
-           _stream(stream))
+           N.ptr(col_ref), ncols if col_ref is not None else 0, _stream(stream))
     return out
 
 
@@ -188,17 +191,25 @@ def records_bucket_capacity(n: int, nstreams: int, nslots: int) -> int:
     return int(N.lib().nvrx_records_bucket_capacity(n, nstreams, nslots))
 
 
-def records_bucket(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: int, stream=None):
+def records_bucket(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: int, stream=None,
+                   out=None):
     """recs: [n, 2] uint32/int32 {slot, ns}; rec_off: [nstreams+1] int64 (device).
-    Returns (seg_off int64 [nstreams*nslots], seg_len int32, out_ns, counts int32)."""
+    Returns (seg_off int64 [nstreams*nslots], seg_len int32, out_ns, counts int32); `out`
+    may pass that tuple preallocated (out_ns >= records_bucket_capacity(...) elements)."""
     nstreams = rec_off.numel() - 1
     dev = recs.device
     n = recs.shape[0]
     cap_ns = records_bucket_capacity(n, nstreams, nslots)
-    seg_off = torch.empty(nstreams * nslots, dtype=torch.int64, device=dev)
-    seg_len = torch.empty(nstreams * nslots, dtype=torch.int32, device=dev)
-    counts = torch.empty(nstreams * nslots, dtype=torch.int32, device=dev)
-    out_ns = torch.empty(max(cap_ns, 1), dtype=torch.int32, device=dev)
+    if out is None:
+        seg_off = torch.empty(nstreams * nslots, dtype=torch.int64, device=dev)
+        seg_len = torch.empty(nstreams * nslots, dtype=torch.int32, device=dev)
+        counts = torch.empty(nstreams * nslots, dtype=torch.int32, device=dev)
+        out_ns = torch.empty(max(cap_ns, 1), dtype=torch.int32, device=dev)
+    else:
+        seg_off, seg_len, out_ns, counts = out
+        if (seg_off.numel() < nstreams * nslots or seg_len.numel() < nstreams * nslots or
+                counts.numel() < nstreams * nslots or out_ns.numel() < cap_ns):
+            raise ValueError("records_bucket: preallocated outputs too small")
     N.call("nvrx_records_bucket", recs.data_ptr(), rec_off.data_ptr(), nstreams, nslots, cap,
            seg_off.data_ptr(), seg_len.data_ptr(), out_ns.data_ptr(), counts.data_ptr(),
            _stream(stream))

@@ -68,6 +68,8 @@ def _load():
         u64 = ctypes.c_uint64
         L.nvrx_synth_matrix.restype = ctypes.c_int
         L.nvrx_synth_matrix.argtypes = [P, i64, i64, i64, P, i64, u64, u64, P, P]
+        L.nvrx_synth_records.restype = ctypes.c_int
+        L.nvrx_synth_records.argtypes = [P, i64, i64, P, P, i64, i64, u64, u64, P, P]
         _lib = L
     return _lib
 
@@ -88,4 +90,44 @@ def synth_matrix(R: int, K_local: int, s_push: int, *, K_global: Optional[int] =
                                    torch.cuda.current_stream(out.device).cuda_stream)
     if rc != 0:
         raise RuntimeError(f"nvrx_synth_matrix failed ({rc})")
+    return out
+
+
+# ---------------------------------------------------------------- record streams (C4)
+def zipf_counts(K: int = 2048, top: int = 8192, alpha: float = 1.1) -> np.ndarray:
+    """Pushes per report interval of kernel k (0-based): max(1, floor(top / (k+1)^alpha))
+    (47,482 records per rank at K=2048)."""
+    k = np.arange(1, K + 1, dtype=np.float64)
+    return np.maximum(1, np.floor(top / k ** alpha)).astype(np.int64)
+
+
+def zipf_order(counts: np.ndarray):
+    """Push order of one rank's interval: occurrence i of kernel k fires at (2i+1)/(2 n_k)
+    of the interval (each kernel evenly spread), ties broken by kernel index.  Distinct
+    fractions with denominators <= 2^15 differ by far more than an f64 ulp, so the f64 key
+    orders them exactly.  Returns (slot uint32 [N], occ uint32 [N])."""
+    counts = np.asarray(counts, np.int64)
+    slot = np.repeat(np.arange(counts.size, dtype=np.int64), counts)
+    first = np.repeat(np.cumsum(counts) - counts, counts)
+    occ = np.arange(slot.size, dtype=np.int64) - first
+    key = (2 * occ + 1) / (2 * counts[slot]).astype(np.float64)
+    order = np.lexsort((slot, key))
+    return slot[order].astype(np.uint32), occ[order].astype(np.uint32)
+
+
+def synth_records(R: int, slot: torch.Tensor, occ: torch.Tensor, K: int, s_push: int, *,
+                  straggler: Optional[torch.Tensor] = None, seed: int = SEED, seed2: int = SEED2,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device record streams, int32 view of {slot, ns} pairs: [R * N, 2], rank-major."""
+    N = slot.numel()
+    dev = slot.device
+    if out is None:
+        out = torch.empty((R * N, 2), dtype=torch.int32, device=dev)
+    if straggler is None:
+        straggler = torch.from_numpy(straggler_ranks(R, seed)).to(dev)
+    rc = _load().nvrx_synth_records(out.data_ptr(), R, N, slot.data_ptr(), occ.data_ptr(), K,
+                                    s_push, seed, seed2, straggler.data_ptr(),
+                                    torch.cuda.current_stream(dev).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"nvrx_synth_records failed ({rc})")
     return out

@@ -65,6 +65,7 @@ def lib():
         L.oracle_ring_linearize.restype = i64
         L.oracle_ring_linearize.argtypes = [P, i64, i64, P]
         L.oracle_matrix_stats.argtypes = [P, i64, i64, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
+        L.oracle_records_stats.argtypes = [P, P, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
         L.oracle_kernel_ref.argtypes = [P, P, i64, i64, P]
         L.oracle_scores.argtypes = [P, P, P, i64, i64, P, P, P, P, P]
         L.oracle_score_partials.argtypes = [P, P, P, i64, i64, P, P, P, P]
@@ -138,6 +139,21 @@ def matrix_stats(ns: np.ndarray, nseg: int, seg_stride: int, seg_begin: int, seg
     lib().oracle_matrix_stats(_p(ns), nseg, seg_stride, seg_begin, seg_len, cap,
                               _p(out["num"]), _p(out["min"]), _p(out["max"]), _p(out["med"]),
                               _p(out["avg"]), _p(out["std"]), int(nthreads))
+    return out
+
+
+def records_stats(recs: np.ndarray, rec_off: np.ndarray, nslots: int, cap: int = 0,
+                  nthreads: int = 1) -> dict:
+    """Stats of every (stream, slot) of push-ordered {slot, ns} record streams
+    (CuptiProfiler.cpp:168-203 ring pushes + getStats), out[t*nslots + s]."""
+    recs = np.ascontiguousarray(recs, dtype=np.uint32).reshape(-1, 2)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.int64)
+    nseg = (rec_off.size - 1) * nslots
+    out = {k: np.empty(nseg, np.int32 if k == "num" else np.float32)
+           for k in ("num", "min", "max", "med", "avg", "std")}
+    lib().oracle_records_stats(_p(recs), _p(rec_off), rec_off.size - 1, nslots, cap,
+                               _p(out["num"]), _p(out["min"]), _p(out["max"]), _p(out["med"]),
+                               _p(out["avg"]), _p(out["std"]), int(nthreads))
     return out
 
 

@@ -65,3 +65,45 @@ def test_sharded_report_matches_single_gpu(ws):
             assert np.array_equal(got["srel"], single[t].stragglers_relative)
             assert np.array_equal(got["sind"], single[t].stragglers_individual)
             assert got["err"] == 0
+
+
+# ---- configs[3] shape: Zipf record streams (bucket by slot -> length-classed stats)
+@pytest.mark.parametrize("R,cap", [(24, 8192), (12, 100), (5, 1)])
+def test_zipf_record_streams_match_oracle(R, cap):
+    K = 2048
+    counts = synth.zipf_counts(K)
+    slot, occ = synth.zipf_order(counts)
+    N = slot.size
+    d_slot = torch.from_numpy(slot.view(np.int32)).cuda()
+    d_occ = torch.from_numpy(occ.view(np.int32)).cuda()
+    recs = synth.synth_records(R, d_slot, d_occ, K, int(counts.max()))
+    rec_off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * N
+    rep = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    res = rep.report_records(recs, rec_off)
+    # oracle: the same streams, ring retention + computeStats per (rank, slot)
+    h = recs.cpu().numpy().view(np.uint32)
+    ref = O.records_stats(h, rec_off.cpu().numpy(), K, cap=cap, nthreads=8)
+    g = rep.stats.cpu()
+    for f in ("num", "min", "max", "med"):
+        a, b = getattr(g, f).numpy(), ref[f]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f
+    small = ref["num"] <= 64  # lane classes: every field bit-exact
+    for f in ("avg", "std"):
+        a, b = getattr(g, f).numpy(), ref[f]
+        assert np.array_equal(a[small].view(np.uint32), b[small].view(np.uint32)), f
+        np.testing.assert_allclose(a, b, rtol=1e-4)
+    num, med, avg = (ref[f].reshape(R, K) for f in ("num", "med", "avg"))
+    gr, gi = O.scores(num, med, avg)
+    np.testing.assert_allclose(res.gpu_relative, gr, rtol=1e-6)
+    np.testing.assert_allclose(res.gpu_individual, gi, rtol=1e-6)
+    assert np.array_equal(res.stragglers_relative, O.stragglers(gr, 0.8).astype(bool))
+    assert np.array_equal(res.stragglers_relative, synth.straggler_ranks(R).astype(bool))
+    assert res.err == 0
+
+
+def test_zipf_order_is_a_valid_interleaving():
+    counts = synth.zipf_counts(2048)
+    assert counts.sum() == 47_482 and counts[0] == 8192 and counts[-1] == 1
+    slot, occ = synth.zipf_order(counts)
+    for k in (0, 1, 7, 100, 2047):
+        assert np.array_equal(occ[slot == k], np.arange(counts[k]))  # push order per kernel

@@ -189,11 +189,11 @@ def test_shape_errors_raise():
         ops.segment_stats_strided(ns, 1, 100, 0, 100, cap=0, mode=7)
 
 
-# ---- the 4-segments-per-wave kernel (segment_rows.hip): strided, stride % 4 == 0, <= 1024 kept
+# ---- short strided segments: every length class up to 1024 kept, all four 16-B phases
 @pytest.mark.parametrize("length", [1, 2, 3, 5, 16, 63, 64, 65, 100, 127, 128, 129, 255, 256, 257,
                                     511, 512, 513, 1000, 1021, 1024])
 @pytest.mark.parametrize("nseg", [4, 5, 7, 33])
-def test_rows_kernel_parity(length, nseg):
+def test_short_segments_parity(length, nseg):
     rng = np.random.default_rng(length * 100 + nseg)
     for begin in (0, 1, 2, 3):
         stride = (length + begin + 3) // 4 * 4 + 4 * int(rng.integers(0, 3))
@@ -205,7 +205,7 @@ def test_rows_kernel_parity(length, nseg):
 
 
 @pytest.mark.parametrize("n", [1, 2, 5, 64, 100, 1024])
-def test_rows_kernel_edge_distributions(n):
+def test_short_segments_edge_distributions(n):
     segs = _edge_segments(n)
     stride = (n + 3) // 4 * 4
     host = np.zeros(len(segs) * stride, np.uint32)
@@ -216,7 +216,7 @@ def test_rows_kernel_edge_distributions(n):
     _check(st, _oracle_segments(host, len(segs), stride, 0, n, 0))
 
 
-def test_rows_kernel_config3_shape_with_colref():
+def test_config3_shape_with_colref():
     # configs[2] shape scaled down: S=1024 per (rank, kernel), and a pushed-1500 / cap-1024 ring
     for S, cap in ((1024, 8192), (1500, 1024)):
         R, K = 9, 24
@@ -229,3 +229,77 @@ def test_rows_kernel_config3_shape_with_colref():
         want = O.kernel_ref(ref["num"].reshape(R, K), ref["med"].reshape(R, K))
         got = col.cpu().numpy()
         assert np.array_equal(got[:K].view(np.float32), want) and not got[K:].any()
+
+
+# ---- classified ragged path (segment_ragged.hip): >= 4096 segments, lengths mixed
+def _mixed_lengths(rng, nseg, longest):
+    u = rng.random(nseg)
+    lens = np.where(u < 0.10, 0,
+           np.where(u < 0.50, rng.integers(1, 9, nseg),
+           np.where(u < 0.70, rng.integers(9, 33, nseg),
+           np.where(u < 0.80, rng.integers(33, 65, nseg),
+           np.where(u < 0.90, rng.integers(65, 1001, nseg),
+           np.where(u < 0.995, rng.integers(1001, 8193, nseg),
+                    rng.integers(8193, longest + 1, nseg)))))))
+    return lens.astype(np.int64)
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_FAST, ops.STATS_EXACT])
+@pytest.mark.parametrize("aligned16", [False, True])
+@pytest.mark.parametrize("cap", [0, 8192, 40])
+def test_ragged_length_classes(mode, aligned16, cap):
+    rng = np.random.default_rng(7 + cap + 2 * aligned16 + 5 * mode)
+    rows, ncols = 60, 80
+    nseg = rows * ncols
+    lens = _mixed_lengths(rng, nseg, 20000)
+    # retained runs start 16-B aligned (aligned16: the promise is about the retained
+    # run, last min(len, cap) samples) or at arbitrary 4-B offsets
+    keeps = np.minimum(lens, cap) if cap > 0 else lens
+    off = np.zeros(nseg, np.int64)
+    pos = 0
+    for s in range(nseg):
+        if aligned16:
+            pos += (-(pos + lens[s] - keeps[s])) % 4
+        else:
+            pos += int(rng.integers(0, 3))
+        off[s] = pos
+        pos += int(lens[s])
+    total = pos + 8
+    host = rng.integers(1000, 5_000_000, size=total, dtype=np.uint32)
+    # a few tightly clustered / duplicate-heavy segments
+    for s in rng.choice(nseg, 50, replace=False):
+        host[off[s]:off[s] + lens[s]] = 777_000 + rng.integers(0, 3, lens[s])
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    col = torch.empty(2 * ncols, dtype=torch.int32, device=DEV)
+    st = ops.segment_stats_ragged(ns, torch.from_numpy(off).to(DEV),
+                                  torch.from_numpy(lens.astype(np.int32)).to(DEV),
+                                  max_len=int(lens.max()), cap=cap, mode=mode,
+                                  aligned16=aligned16, col_ref=col, ncols=ncols)
+    g = st.cpu()
+    num = np.empty(nseg, np.int32)
+    med = np.empty(nseg, np.float32)
+    for s in range(nseg):
+        L = int(lens[s])
+        seg = host[off[s]:off[s] + L]
+        keep = min(L, cap) if cap > 0 else L
+        r = O.compute_stats(O.ns_to_us(seg[L - keep:]))
+        num[s], med[s] = r.num_calls, r.median
+        if keep == 0:
+            assert g.num[s].item() == 0 and np.isnan(g.med[s].item()) and np.isnan(g.std[s].item())
+            continue
+        got = [np.float32(getattr(g, f)[s].item()) for f in ("min", "max", "med", "avg", "std")]
+        want = [np.float32(x) for x in (r.min, r.max, r.median, r.avg, r.stddev)]
+        assert g.num[s].item() == r.num_calls, s
+        assert got[:3] == want[:3], (s, keep, got, want)
+        if mode == ops.STATS_EXACT or keep <= 64:  # lane / workgroup classes: every field
+            assert got[3:] == want[3:], (s, keep, got, want)
+        else:
+            v = seg[L - keep:].astype(np.float64)
+            assert abs(got[3] - v.mean() / 1000) <= 2.5e-7 * v.mean() / 1000 or got[3] == want[3], s
+            assert abs(got[4] - v.std() / 1000) <= 1e-6 * v.std() / 1000 + 1e-6 or got[4] == want[4], s
+    want_ref = O.kernel_ref(num.reshape(rows, ncols), med.reshape(rows, ncols))
+    c = col.cpu().numpy()
+    missing = c[ncols:] != 0
+    assert np.array_equal(missing, (num.reshape(rows, ncols) == 0).any(axis=0))
+    ok = ~missing
+    assert np.array_equal(c[:ncols].view(np.float32)[ok], want_ref[ok])
