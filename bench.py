@@ -11,7 +11,9 @@ Workload (value): BASELINE configs[1] per GPU -- 64 simulated ranks x 2048 kerne
 kernel columns are sharded by hash(kernel name) % N with 2048*N kernels in total (weak
 scaling); the only exchange is one RCCL all_gather of [64][6] f64 score partials.
 Secondary: report latency at 4096 ranks (configs[2]: 4096 x 2048 x 1024 samples, the
-same 2048 kernels split over the N GPUs).
+same 2048 kernels split over the N GPUs), and configs[3]: Zipf record streams at 16,384
+simulated ranks (47,482 {slot, ns} records per rank, kernel k pushed floor(8192/k^1.1)
+times, 1.3x stragglers) -> bucket by slot -> length-classed stats -> scores.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 (N > 1: launched by torch.distributed.run, one process per GPU.)
@@ -36,6 +38,8 @@ HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip table (spec)
 THR = 0.8          # a 1.3x straggler scores ~0.77 (> the 0.75 default)
 C2 = dict(R=64, K=2048, s_push=10000, cap=8192)
 C3 = dict(R=4096, K=2048, s_push=1024, cap=8192)
+C4 = dict(R=16384, K=2048, cap=8192)
+RECORD_BYTES = 8  # {u32 slot, u32 ns}
 STATS_BYTES_PER_SEGMENT = 24  # num/min/max/med/avg/std written per segment
 
 
@@ -102,6 +106,67 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True)
                 samples=R * K_local * keep, nseg=R * K_local, keep=keep)
 
 
+def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
+    """configs[3]: record streams of R ranks (kernels sharded by name hash over N GPUs, the
+    whole R on every GPU), one full report per step."""
+    R, K, cap = C4["R"], C4["K"], C4["cap"]
+    counts = synth.zipf_counts(K)
+    slot, occ = synth.zipf_order(counts)
+    names = synth.kernel_names(K)
+    kidx = synth.shard_kernels(names, world, rank) if world > 1 else np.arange(K)
+    lslot, kglob, locc = synth.shard_order(slot, occ, kidx)
+    N = lslot.size
+    t = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)
+    recs = synth.synth_records(R, t(lslot), t(locc), K, int(counts.max()), kglob=t(kglob))
+    rec_off = torch.arange(R + 1, dtype=torch.int64, device=dev) * N
+    rep = batch.MatrixReporter(R, len(kidx), cap=cap, thr_rel=THR, thr_ind=THR, device=dev)
+    for _ in range(warmup):
+        res = rep.report_records(recs, rec_off)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record()
+        rep.compute_stats_records(recs, rec_off)
+        ev[i][1].record()
+        rep.compute_scores()
+        res = rep.land()
+        ev[i][2].record()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    stats_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    tmax = allreduce(elapsed, torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
+    nrec = allreduce(float(R * N), torch.distributed.ReduceOp.SUM if world > 1 else None, world, dev)
+    out = dict(ranks=R, kernels=K, records_per_rank=int(counts.sum()), cap=cap,
+               ms_per_report=tmax / steps * 1e3, records_per_s=nrec * steps / tmax,
+               bucket_plus_stats_ms=stats_ms,
+               hbm_frac_of_report=R * N * RECORD_BYTES / (tmax / steps) / HBM_PEAK,
+               hbm_frac_of_stats=R * N * RECORD_BYTES / (stats_ms * 1e-3) / HBM_PEAK,
+               alg_bytes_per_record=RECORD_BYTES,
+               straggler_sets_exact=bool(np.array_equal(
+                   res.stragglers_relative, synth.straggler_ranks(R).astype(bool))))
+    if world == 1 and rank == 0 and cpu_ranks > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        h = recs[:cpu_ranks * N].cpu().numpy().view(np.uint32)
+        off = np.arange(cpu_ranks + 1, dtype=np.int64) * N
+        t1 = time.perf_counter()
+        st = O.records_stats(h, off, K, cap=cap, nthreads=threads)
+        gr, gi = O.scores(st["num"].reshape(cpu_ranks, K), st["med"].reshape(cpu_ranks, K),
+                          st["avg"].reshape(cpu_ranks, K))
+        O.stragglers(gr, THR)
+        dt = time.perf_counter() - t1
+        g = rep.stats
+        n = cpu_ranks * K
+        parity = all(np.array_equal(getattr(g, f)[:n].cpu().numpy().view(np.int32), st[f].view(np.int32))
+                     for f in ("num", "min", "max", "med"))
+        out["cpu_baseline"] = dict(value=cpu_ranks * N / dt, unit="records/s", cores=threads,
+                                   kind="port", sample=f"{cpu_ranks} of {R} ranks ({cpu_ranks * N} "
+                                   f"records, {dt:.2f} s): oracle C ring-push + computeStats + "
+                                   f"scoring restatement", gpu_stats_bit_exact_on_sample=parity)
+    return out
+
+
 def pmc_traffic(workload: str):
     """HBM bytes per launch of the stats kernel from a committed rocprofv3 --pmc summary
     (profiles/pmc_<workload>.json, corrected per MI355X_MICROARCH.md: FETCH_SIZE x2)."""
@@ -151,6 +216,8 @@ def main():
     ap.add_argument("--no-latency4096", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-ranks", type=int, default=16)
+    ap.add_argument("--no-zipf", action="store_true")
+    ap.add_argument("--zipf-cpu-ranks", type=int, default=128)
     args = ap.parse_args()
     rank, world, dev = dist_setup()
     if world != args.gpus:
@@ -191,11 +258,19 @@ def main():
         del r4
         torch.cuda.empty_cache()
 
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    # ---------------- configs[3]: Zipf record streams at 16k ranks --------------------
+    zipf = None
+    if not args.no_zipf:
+        torch.cuda.empty_cache()
+        zipf = run_zipf(max(3, args.steps // 4), 2, world, rank, dev,
+                        0 if args.no_cpu_baseline else args.zipf_cpu_ranks, threads)
+        torch.cuda.empty_cache()
+
     # ---------------- CPU baseline (rank 0, N == 1 only) ------------------------------
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-        threads = max(1, min(threads, len(os.sched_getaffinity(0))))
         ns_c2, kidx = make_shard(C2["R"], C2["K"], C2["s_push"], 1, 0, dev)
         rep = batch.MatrixReporter(C2["R"], len(kidx), cap=C2["cap"], device=dev)
         rep.compute_stats(ns_c2, C2["s_push"])
@@ -236,6 +311,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,
+            "zipf_16384_ranks": zipf,
             "straggler_sets_exact": sets_ok,
         }
         print(json.dumps(line), flush=True)

@@ -46,6 +46,7 @@ extern "C" {
 #define NVRX_ERR_STATE -3     /* call not valid in the current state */
 #define NVRX_ERR_SINGLETON -4 /* a second profiler instance (CuptiProfiler.cpp:86-87) */
 #define NVRX_ERR_NOMEM -5
+#define NVRX_ERR_RUNTIME -6 /* rocprofiler-sdk / runtime configuration refused */
 
 /* statistics modes */
 #define NVRX_STATS_FAST 0  /* NUM/MIN/MAX/MED bit-exact; AVG/STD exact mean/std rounded once to f32 */
@@ -219,7 +220,14 @@ int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, u
                             int32_t* num, float* mn, float* mx, float* med, float* avg,
                             float* sd);
 int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_t buflen);
-/* Live kernel-dispatch capture through rocprofiler-sdk (0 = not available). */
+/* Live kernel-dispatch capture through rocprofiler-sdk (CuptiProfiler.cpp:96-203).
+ * nvrx_capture_configure registers the library as a rocprofiler-sdk tool; it must run
+ * before the process's first HIP call (NVRX_ERR_STATE otherwise).  Once the runtime has
+ * initialised, nvrx_profiler_capture_available() returns 1 and every kernel that completes
+ * while a profiler handle is started is pushed into it under the reference's composite key
+ * "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled name, block dims, grid dims in blocks) with its
+ * integer-ns duration; nvrx_profiler_stop / _get_stats flush the capture buffer first. */
+int nvrx_capture_configure(void);
 int nvrx_profiler_capture_available(void);
 
 #ifdef __cplusplus

@@ -19,10 +19,11 @@ int nvrx_synth_matrix(uint32_t* out, int64_t R, int64_t K_local, int64_t K_globa
                       const int64_t* kmap, int64_t s_push, uint64_t seed, uint64_t seed2,
                       const uint8_t* straggler, void* stream);
 /* Record streams (configs[3]): out[r*N + j] = {slot[j], ns}, ns the occ[j]-th sample of
- * kernel slot[j] on rank r under the hash above with S_push = s_push, K = K. */
+ * global kernel kglob[j] (kglob NULL: slot[j]) on rank r under the hash above with
+ * S_push = s_push and K = K (the global kernel count). */
 int nvrx_synth_records(uint32_t* out, int64_t R, int64_t N, const uint32_t* slot,
-                       const uint32_t* occ, int64_t K, int64_t s_push, uint64_t seed,
-                       uint64_t seed2, const uint8_t* straggler, void* stream);
+                       const uint32_t* kglob, const uint32_t* occ, int64_t K, int64_t s_push,
+                       uint64_t seed, uint64_t seed2, const uint8_t* straggler, void* stream);
 #ifdef __cplusplus
 }
 #endif

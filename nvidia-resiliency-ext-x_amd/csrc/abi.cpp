@@ -40,6 +40,10 @@ hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace
 
+namespace nvrx {
+void set_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace nvrx
+
 extern "C" {
 
 const char* nvrx_last_error(void) { return g_last_error.c_str(); }
@@ -373,6 +377,24 @@ int flush_locked(nvrx_profiler* p) {
 
 }  // namespace
 
+namespace nvrx {
+// capture.cpp's dispatch callback: one completed kernel under its composite key
+void profiler_push_named(nvrx_profiler* p, const char* key, uint32_t ns) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->started) return;
+    auto it = p->name_to_slot.find(key);
+    uint32_t slot;
+    if (it != p->name_to_slot.end()) {
+        slot = it->second;
+    } else {
+        slot = (uint32_t)p->names.size();
+        p->name_to_slot.emplace(key, slot);
+        p->names.emplace_back(key);
+    }
+    p->staged.push_back(nvrx_record{slot, ns});
+}
+}  // namespace nvrx
+
 extern "C" {
 
 int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
@@ -402,6 +424,7 @@ int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
 
 int nvrx_profiler_destroy(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_destroy: null handle");
+    nvrx::capture_detach(p);
     {
         std::lock_guard<std::mutex> lk(g_instance_mu);
         if (g_instance == p) g_instance = nullptr;
@@ -437,17 +460,26 @@ int nvrx_profiler_shutdown(nvrx_profiler* p) {
 
 int nvrx_profiler_start(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_start: null handle");
-    std::lock_guard<std::mutex> lk(p->mu);
-    if (p->started) std::fprintf(stderr, "CuptiProfiler::startProfiling subsequent call.\n");
-    p->started = true;
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        if (p->started) std::fprintf(stderr, "CuptiProfiler::startProfiling subsequent call.\n");
+        p->started = true;
+    }
+    // live capture (CuptiProfiler.cpp:115-118 enables the activity kind)
+    if (nvrx::capture_start(p) != 0)
+        return fail(NVRX_ERR_STATE, "nvrx_profiler_start: rocprofiler_start_context failed");
     return NVRX_OK;
 }
 
 int nvrx_profiler_stop(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_stop: null handle");
+    // deliver the dispatches that completed while started, outside the handle lock (the
+    // buffer callback takes it)
+    const int rc = nvrx::capture_stop(p);
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->started) std::fprintf(stderr, "CuptiProfiler::stopProfiling called while not profiling.\n");
     p->started = false;
+    if (rc != 0) return fail(NVRX_ERR_STATE, "nvrx_profiler_stop: rocprofiler_stop_context failed");
     return NVRX_OK;
 }
 
@@ -488,6 +520,7 @@ int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n) {
 int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
                             int32_t* num, float* mn, float* mx, float* med, float* avg, float* sd) {
     NVRX_CHECK_ARG(p && count, "nvrx_profiler_get_stats: null argument");
+    (void)nvrx::capture_flush();  // CuptiProfiler.cpp:138 cuptiActivityFlushAll (before the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);
     int rc = flush_locked(p);

@@ -1,5 +1,188 @@
-// capture.cpp -- live kernel-dispatch capture (rocprofiler-sdk) for the profiler handle.
-// Round 1: not wired yet; records enter through nvrx_profiler_push.
+// capture.cpp -- live kernel-dispatch capture through rocprofiler-sdk (replaces the CUPTI
+// activity path of nvrx_cupti_module: CuptiProfiler.cpp:96-203).
+//
+// The reference enables CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL, receives activity buffers on
+// CUPTI's thread and, per record, builds the key "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled
+// kernel name, block dims, grid dims in blocks) and pushes (end - start) / 1000.0f into that
+// key's ring.  Here a rocprofiler-sdk tool owns two contexts:
+//   * "symbols"  (started at configuration): code-object callback tracing, kernel_id -> name;
+//   * "dispatch" (started / stopped with the profiler handle): buffer tracing of
+//     ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH.
+// The buffer callback turns each completed dispatch into the reference's key (workgroup
+// size = block dims; grid_size is in work-items, so blocks = grid_size / workgroup_size) and
+// an integer-ns duration record appended to the profiler handle's record log; the per-key
+// rings and statistics are then the HIP kernels of the report path.
+//
+// rocprofiler-sdk tools configure when the ROCm runtime initialises: nvrx_capture_configure
+// must run before the process's first HIP call (the Python side does it at
+// KernelProfiler(capture=True) construction and reports whether it took effect).
+#include <rocprofiler-sdk/registration.h>
+#include <rocprofiler-sdk/rocprofiler.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
 #include "nvrx_internal.h"
 
-extern "C" int nvrx_profiler_capture_available(void) { return 0; }
+namespace {
+
+struct Capture {
+    std::mutex mu;
+    std::unordered_map<uint64_t, std::string> names;  // kernel_id -> kernel name
+    rocprofiler_context_id_t sym_ctx{0};
+    rocprofiler_context_id_t disp_ctx{0};
+    rocprofiler_buffer_id_t buffer{0};
+    std::atomic<bool> ready{false};      // tool_init completed
+    std::atomic<bool> requested{false};  // nvrx_capture_configure succeeded
+    std::atomic<nvrx_profiler*> target{nullptr};
+    rocprofiler_client_id_t* client = nullptr;
+};
+
+Capture& cap() {
+    static Capture c;
+    return c;
+}
+
+void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_user_data_t*,
+                    void*) {
+    if (record.kind != ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT ||
+        record.operation != ROCPROFILER_CODE_OBJECT_DEVICE_KERNEL_SYMBOL_REGISTER ||
+        record.phase != ROCPROFILER_CALLBACK_PHASE_LOAD)
+        return;
+    auto* d = static_cast<rocprofiler_callback_tracing_code_object_kernel_symbol_register_data_t*>(
+        record.payload);
+    std::string n = d->kernel_name ? d->kernel_name : "";
+    if (n.size() > 3 && n.compare(n.size() - 3, 3, ".kd") == 0) n.resize(n.size() - 3);
+    std::lock_guard<std::mutex> lk(cap().mu);
+    cap().names[d->kernel_id] = std::move(n);
+}
+
+void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
+                        rocprofiler_record_header_t** headers, size_t num_headers, void*,
+                        uint64_t) {
+    nvrx_profiler* p = cap().target.load();
+    if (!p) return;
+    char key[4096];
+    for (size_t i = 0; i < num_headers; ++i) {
+        const rocprofiler_record_header_t* h = headers[i];
+        if (h->category != ROCPROFILER_BUFFER_CATEGORY_TRACING ||
+            h->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
+            continue;
+        auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
+        const rocprofiler_kernel_dispatch_info_t& di = r->dispatch_info;
+        std::string name;
+        {
+            std::lock_guard<std::mutex> lk(cap().mu);
+            auto it = cap().names.find(di.kernel_id);
+            name = it != cap().names.end() ? it->second : std::string("unknown_kernel");
+        }
+        const uint32_t bx = di.workgroup_size.x, by = di.workgroup_size.y, bz = di.workgroup_size.z;
+        const uint32_t gx = bx ? di.grid_size.x / bx : 0, gy = by ? di.grid_size.y / by : 0,
+                       gz = bz ? di.grid_size.z / bz : 0;
+        // CuptiProfiler.cpp:182-185
+        std::snprintf(key, sizeof(key), "%s_blk_%d_%d_%d_grid_%d_%d_%d", name.c_str(), (int)bx,
+                      (int)by, (int)bz, (int)gx, (int)gy, (int)gz);
+        const uint64_t dt = r->end_timestamp > r->start_timestamp
+                                ? r->end_timestamp - r->start_timestamp
+                                : 0;
+        nvrx::profiler_push_named(p, key, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt);
+    }
+}
+
+int tool_init(rocprofiler_client_finalize_t, void*) {
+    Capture& c = cap();
+    if (rocprofiler_create_context(&c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+    if (rocprofiler_configure_callback_tracing_service(c.sym_ctx,
+                                                       ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT,
+                                                       nullptr, 0, code_object_cb,
+                                                       nullptr) != ROCPROFILER_STATUS_SUCCESS)
+        return -1;
+    if (rocprofiler_create_context(&c.disp_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+    if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, 6u << 20, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
+                                  dispatch_buffer_cb, nullptr, &c.buffer) != ROCPROFILER_STATUS_SUCCESS)
+        return -1;
+    if (rocprofiler_configure_buffer_tracing_service(c.disp_ctx,
+                                                     ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH,
+                                                     nullptr, 0, c.buffer) != ROCPROFILER_STATUS_SUCCESS)
+        return -1;
+    if (rocprofiler_start_context(c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+    c.ready = true;
+    return 0;
+}
+
+void tool_fini(void*) {
+    Capture& c = cap();
+    if (!c.ready) return;
+    (void)rocprofiler_flush_buffer(c.buffer);
+    c.ready = false;
+}
+
+rocprofiler_tool_configure_result_t* nvrx_tool_configure(uint32_t, const char*, uint32_t,
+                                                         rocprofiler_client_id_t* id) {
+    id->name = "nvrx-straggler";
+    cap().client = id;
+    static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t),
+                                                   &tool_init, &tool_fini, nullptr};
+    return &cfg;
+}
+
+}  // namespace
+
+namespace nvrx {
+
+bool capture_ready() { return cap().ready.load(); }
+
+int capture_start(nvrx_profiler* p) {
+    Capture& c = cap();
+    if (!c.ready) return 0;
+    c.target.store(p);
+    return rocprofiler_start_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
+}
+
+int capture_stop(nvrx_profiler* p) {
+    Capture& c = cap();
+    if (!c.ready) return 0;
+    int rc = rocprofiler_stop_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
+    (void)rocprofiler_flush_buffer(c.buffer);  // deliver what completed while started
+    (void)p;
+    return rc;
+}
+
+int capture_flush() {
+    Capture& c = cap();
+    if (!c.ready) return 0;
+    return rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
+}
+
+void capture_detach(nvrx_profiler* p) {
+    Capture& c = cap();
+    nvrx_profiler* cur = p;
+    if (c.target.compare_exchange_strong(cur, nullptr) && c.ready)
+        (void)rocprofiler_stop_context(c.disp_ctx);
+}
+
+}  // namespace nvrx
+
+extern "C" {
+
+int nvrx_capture_configure(void) {
+    Capture& c = cap();
+    if (c.requested || c.ready) return NVRX_OK;
+    const rocprofiler_status_t st = rocprofiler_force_configure(&nvrx_tool_configure);
+    if (st != ROCPROFILER_STATUS_SUCCESS) {
+        nvrx::set_error(std::string("nvrx_capture_configure: rocprofiler_force_configure: ") +
+                        rocprofiler_get_status_string(st) +
+                        " (capture must be configured before the first HIP call)");
+        return NVRX_ERR_RUNTIME;
+    }
+    c.requested = true;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_capture_available(void) { return cap().ready.load() ? 1 : 0; }
+
+}  // extern "C"

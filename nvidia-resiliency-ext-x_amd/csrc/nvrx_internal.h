@@ -41,4 +41,14 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
 hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, const int64_t* dst_off,
                             const uint32_t* ns, int64_t nslots, nvrx_record* out, hipStream_t st);
 
+// abi.cpp <-> capture.cpp
+#include <string>
+void set_error(const std::string& msg);
+void profiler_push_named(nvrx_profiler* p, const char* key, uint32_t ns);
+bool capture_ready();
+int capture_start(nvrx_profiler* p);
+int capture_stop(nvrx_profiler* p);
+int capture_flush();
+void capture_detach(nvrx_profiler* p);
+
 }  // namespace nvrx

@@ -56,20 +56,21 @@ __global__ void synth_matrix_kernel(uint32_t* out, int64_t R, int64_t K_local, i
 // record streams: out[r*N + j] = {slot[j], ns(r, slot[j], occ[j])}, the occ[j]-th push of
 // kernel slot[j] on rank r (same sample hash as the matrix with S_push = s_push)
 __global__ void synth_records_kernel(uint32_t* out, int64_t R, int64_t N, const uint32_t* slot,
-                                     const uint32_t* occ, int64_t K, int64_t s_push, uint64_t seed,
-                                     uint64_t seed2, const uint8_t* straggler) {
+                                     const uint32_t* kglob, const uint32_t* occ, int64_t K,
+                                     int64_t s_push, uint64_t seed, uint64_t seed2,
+                                     const uint8_t* straggler) {
     const int64_t total = R * N;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = e / N;
         const int64_t j = e - r * N;
-        const uint64_t k = slot[j];
+        const uint64_t k = kglob ? kglob[j] : slot[j];
         const uint64_t base = 2000ull + splitmix64(seed2 ^ k) % 1998000ull;
         const uint64_t u = splitmix64(seed ^ (((uint64_t)r * (uint64_t)K + k) * (uint64_t)s_push +
                                               (uint64_t)occ[j]));
         uint64_t ns = base + (((u >> 32) * (base / 10ull)) >> 32);
         if (straggler && straggler[r]) ns = ns * 13ull / 10ull;
-        out[2 * e] = (uint32_t)k;
+        out[2 * e] = slot[j];
         out[2 * e + 1] = (uint32_t)ns;
     }
 }
@@ -77,15 +78,17 @@ __global__ void synth_records_kernel(uint32_t* out, int64_t R, int64_t N, const 
 }  // namespace
 
 extern "C" int nvrx_synth_records(uint32_t* out, int64_t R, int64_t N, const uint32_t* slot,
-                                  const uint32_t* occ, int64_t K, int64_t s_push, uint64_t seed,
-                                  uint64_t seed2, const uint8_t* straggler, void* stream) {
+                                  const uint32_t* kglob, const uint32_t* occ, int64_t K,
+                                  int64_t s_push, uint64_t seed, uint64_t seed2,
+                                  const uint8_t* straggler, void* stream) {
     if (!out || !slot || !occ || R < 0 || N < 0) return -1;
     const int64_t total = R * N;
     if (total == 0) return 0;
     int64_t blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(synth_records_kernel, dim3((unsigned)blocks), dim3(256), 0,
-                       (hipStream_t)stream, out, R, N, slot, occ, K, s_push, seed, seed2, straggler);
+                       (hipStream_t)stream, out, R, N, slot, kglob, occ, K, s_push, seed, seed2,
+                       straggler);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

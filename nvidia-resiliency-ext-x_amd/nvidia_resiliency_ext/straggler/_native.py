@@ -64,6 +64,7 @@ class ProfilerConfig(ctypes.Structure):
 # name -> (restype, argtypes); every symbol the header declares
 SIGNATURES = {
     "nvrx_last_error": (ctypes.c_char_p, []),
+    "nvrx_capture_configure": (ctypes.c_int, []),
     "nvrx_abi_version": (ctypes.c_int, []),
     "nvrx_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "nvrx_sync": (ctypes.c_int, [P]),

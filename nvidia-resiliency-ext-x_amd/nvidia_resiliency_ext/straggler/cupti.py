@@ -4,15 +4,21 @@
 (cupti_module_py.cpp:33-54) with the nvrx_profiler handle of libnvrx_hip.so: records are
 kept as a device-resident log in HBM and reduced to per-kernel statistics by the HIP
 kernels at get_stats time (only the last ``statsMaxLenPerKernel`` records of every kernel
-count, as the reference's rings keep them).  Records enter through ``push`` (and, when
-available, the rocprofiler-sdk kernel-dispatch capture).
+count, as the reference's rings keep them).  Records enter through the rocprofiler-sdk
+kernel-dispatch capture (capture.cpp: every kernel that completes while the profiler is
+started, keyed like CuptiProfiler.cpp:182-185) and through ``push`` (external tracers,
+tests).  rocprofiler-sdk tools configure when the ROCm runtime initialises, so capture
+needs ``enable_capture()`` (or the first ``KernelProfiler``) before the process's first
+HIP call -- the same constraint CUPTI activity tracing has on its first CUDA context.
 
 ``CuptiManager`` keeps the reference's thread-safe, refcounted start/stop semantics.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
+import warnings
 from typing import Dict, Iterable, Optional, Sequence
 
 import numpy as np
@@ -36,12 +42,39 @@ class KernelStats:
                 f"{self.median}, avg: {self.avg}, stddev: {self.stddev}")
 
 
+_capture_state: Optional[bool] = None
+
+
+def enable_capture() -> bool:
+    """Register the rocprofiler-sdk kernel-dispatch tool (idempotent).  Returns False when
+    the ROCm runtime of this process is already initialised (capture then unavailable;
+    records can still be pushed).  NVRX_CAPTURE=0 disables it."""
+    global _capture_state
+    if _capture_state is None:
+        if os.environ.get("NVRX_CAPTURE", "1") == "0":
+            _capture_state = False
+        else:
+            _capture_state = N.lib().nvrx_capture_configure() == 0
+    return _capture_state
+
+
+def capture_available() -> bool:
+    """True once the runtime has initialised with the capture tool configured."""
+    return bool(N.lib().nvrx_profiler_capture_available())
+
+
 class KernelProfiler:
     """nvrx_cupti_module.CuptiProfiler(bufferSize, numBuffers, statsMaxLenPerKernel)."""
 
     def __init__(self, bufferSize: int = 1024 * 1024 * 8, numBuffers: int = 8,
                  statsMaxLenPerKernel: int = 1024, device: Optional[int] = None,
-                 exact: bool = True):
+                 exact: bool = True, capture: bool = True):
+        if capture and not enable_capture() and _capture_state is False and \
+                os.environ.get("NVRX_CAPTURE", "1") != "0":
+            warnings.warn("kernel-dispatch capture unavailable: the ROCm runtime was initialised "
+                          "before the straggler profiler (call nvidia_resiliency_ext.straggler."
+                          "cupti.enable_capture() first); only pushed records are profiled",
+                          RuntimeWarning, stacklevel=2)
         if device is None:
             import torch
 
@@ -119,8 +152,25 @@ class KernelProfiler:
         p = lambda a: a.ctypes.data  # noqa: E731
         N.check(L.nvrx_profiler_get_stats(self._h, n, ctypes.byref(count), p(slots), p(num),
                                           *(p(c) for c in cols)), "get_stats")
-        names = [self._names[s] for s in slots]
+        names = [self._name_of(int(s)) for s in slots]
         return KernelSummaries(names, num, *cols)
+
+    def _name_of(self, s: int) -> str:
+        """Slot -> composite name; slots created by the capture callback are fetched once."""
+        if s < len(self._names) and self._names[s] is not None:
+            return self._names[s]
+        buf = ctypes.create_string_buffer(8192)
+        N.call("nvrx_profiler_kernel_name", self._h, s, buf, len(buf))
+        name = buf.value.decode()
+        while len(self._names) <= s:
+            self._names.append(None)
+        self._names[s] = name
+        self._slot_of[name] = s
+        return name
+
+    @property
+    def capture(self) -> bool:
+        return capture_available()
 
     def get_stats(self) -> Dict[str, KernelStats]:
         ks = self.get_stats_columns()

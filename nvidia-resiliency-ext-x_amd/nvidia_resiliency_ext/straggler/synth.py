@@ -69,7 +69,7 @@ def _load():
         L.nvrx_synth_matrix.restype = ctypes.c_int
         L.nvrx_synth_matrix.argtypes = [P, i64, i64, i64, P, i64, u64, u64, P, P]
         L.nvrx_synth_records.restype = ctypes.c_int
-        L.nvrx_synth_records.argtypes = [P, i64, i64, P, P, i64, i64, u64, u64, P, P]
+        L.nvrx_synth_records.argtypes = [P, i64, i64, P, P, P, i64, i64, u64, u64, P, P]
         _lib = L
     return _lib
 
@@ -116,18 +116,32 @@ def zipf_order(counts: np.ndarray):
 
 
 def synth_records(R: int, slot: torch.Tensor, occ: torch.Tensor, K: int, s_push: int, *,
-                  straggler: Optional[torch.Tensor] = None, seed: int = SEED, seed2: int = SEED2,
+                  kglob: Optional[torch.Tensor] = None, straggler: Optional[torch.Tensor] = None,
+                  seed: int = SEED, seed2: int = SEED2,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Device record streams, int32 view of {slot, ns} pairs: [R * N, 2], rank-major."""
+    """Device record streams, int32 view of {slot, ns} pairs: [R * N, 2], rank-major.
+    kglob (optional, [N]): global kernel index of each record for the sample hash when
+    `slot` holds shard-local slots (K is then the global kernel count)."""
     N = slot.numel()
     dev = slot.device
     if out is None:
         out = torch.empty((R * N, 2), dtype=torch.int32, device=dev)
     if straggler is None:
         straggler = torch.from_numpy(straggler_ranks(R, seed)).to(dev)
-    rc = _load().nvrx_synth_records(out.data_ptr(), R, N, slot.data_ptr(), occ.data_ptr(), K,
-                                    s_push, seed, seed2, straggler.data_ptr(),
+    rc = _load().nvrx_synth_records(out.data_ptr(), R, N, slot.data_ptr(),
+                                    kglob.data_ptr() if kglob is not None else None,
+                                    occ.data_ptr(), K, s_push, seed, seed2, straggler.data_ptr(),
                                     torch.cuda.current_stream(dev).cuda_stream)
     if rc != 0:
         raise RuntimeError(f"nvrx_synth_records failed ({rc})")
     return out
+
+
+def shard_order(slot: np.ndarray, occ: np.ndarray, kidx: np.ndarray):
+    """Restrict a push order to the kernels `kidx` (global indices, this shard), keeping
+    push order; returns (local slot, global kernel, occ), all uint32."""
+    local = np.full(int(slot.max()) + 1 if slot.size else 1, -1, np.int64)
+    local[kidx] = np.arange(kidx.size)
+    keep = local[slot.astype(np.int64)] >= 0
+    g = slot[keep]
+    return local[g.astype(np.int64)].astype(np.uint32), g.astype(np.uint32), occ[keep]

@@ -1,0 +1,73 @@
+"""GPU: live kernel-dispatch capture through rocprofiler-sdk (capture.cpp), the replacement
+of the CUPTI activity path (CuptiProfiler.cpp:96-203; test_cupti_ext.py's capture checks).
+
+rocprofiler-sdk tools configure when the ROCm runtime initialises, so each case runs in a
+fresh child process that creates the profiler before its first HIP call."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, sys
+sys.path.insert(0, %(pkg)r)
+from nvidia_resiliency_ext.straggler import cupti, ops
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=%(cap)d, capture=True)
+out = {"available": cupti.capture_available()}
+p.initialize()
+p.start()
+x = torch.randn(256, 256, device="cuda")
+for _ in range(5):
+    y = x @ x
+score = torch.rand(1000, dtype=torch.float64, device="cuda")
+for _ in range(%(nstrag)d):
+    ops.stragglers(score, 0.5)
+torch.cuda.synchronize()
+p.stop()
+for _ in range(3):
+    ops.stragglers(score, 0.5)  # stopped: not captured
+torch.cuda.synchronize()
+out["stats"] = {k: [v.num_calls, v.min, v.median, v.max] for k, v in p.get_stats().items()}
+p.reset()
+out["after_reset"] = len(p.get_stats())
+print("RESULT " + json.dumps(out))
+"""
+
+
+def _run(cap, nstrag):
+    code = CHILD % dict(pkg=os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"), cap=cap, nstrag=nstrag)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1]
+    return json.loads(line[len("RESULT "):])
+
+
+def test_dispatch_capture_keys_counts_and_start_stop():
+    out = _run(cap=64, nstrag=7)
+    assert out["available"]
+    stats = out["stats"]
+    key_re = re.compile(r"^(.+)_blk_(\d+)_(\d+)_(\d+)_grid_(\d+)_(\d+)_(\d+)$")
+    assert stats and all(key_re.match(k) for k in stats), list(stats)[:5]
+    strag = {k: v for k, v in stats.items() if "stragglers" in k}
+    assert len(strag) == 1, list(stats)
+    (k, (num, mn, med, mx)), = strag.items()
+    assert num == 7                        # the 3 launches after stop() are not captured
+    assert 0 < mn <= med <= mx < 1e5       # microseconds
+    # torch's GEMM: 5 launches (one key per distinct launch shape)
+    assert sum(v[0] for kk, v in stats.items() if "stragglers" not in kk) >= 5
+    assert list(stats) == sorted(stats)    # std::map order (CuptiProfiler.cpp:137-145)
+    assert out["after_reset"] == 0
+
+
+def test_dispatch_capture_ring_cap():
+    # statsMaxLenPerKernel=4: only the last 4 dispatches of a kernel count (num_calls == 4)
+    out = _run(cap=4, nstrag=9)
+    strag = [v for k, v in out["stats"].items() if "stragglers" in k]
+    assert strag and strag[0][0] == 4
