@@ -18,6 +18,10 @@
 //           overflowed slots are placed by wave 0 alone, in push order: 64 records per
 //           step, same-slot lanes grouped with ballot (leader = lowest lane), occurrence
 //           index = cursor + mbcnt(group), kept iff occurrence >= count - keep.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
@@ -32,26 +36,48 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
     return ((rec_off[t] + 3) & ~(int64_t)3) + t * stream_slack(nslots);
 }
 
-constexpr int RB_WAVES = 4;
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
 
-// records [lo, hi) of a stream in 16-byte pairs where the base allows it; f(rec) per record
+// records [lo, hi) of a stream in 16-byte pairs where the base allows it; f(rec) per record.
+// RB_UNROLL independent loads per lane are issued before any is consumed: a wave keeps
+// RB_UNROLL KB in flight instead of one (the loop is otherwise latency-bound).
+constexpr int RB_UNROLL = 8;
 template <class F>
 __device__ __forceinline__ void for_records(const nvrx_record* rs, int64_t lo, int64_t hi, int lane,
                                             bool pairs, F&& f) {
     if (pairs) {  // lo, hi even; rs 16-B aligned
-        const uint4* q = (const uint4*)(rs + lo);
+        const u32x4* q = (const u32x4*)(rs + lo);
         const int64_t np = (hi - lo) >> 1;
-        for (int64_t i = lane; i < np; i += 64) {
-            const uint4 w = q[i];
+        int64_t i = lane;
+        for (; i + 64 * (RB_UNROLL - 1) < np; i += 64 * RB_UNROLL) {
+            u32x4 w[RB_UNROLL];
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) w[u] = __builtin_nontemporal_load(q + i + 64 * u);
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) {
+                f(nvrx_record{w[u].x, w[u].y});
+                f(nvrx_record{w[u].z, w[u].w});
+            }
+        }
+        for (; i < np; i += 64) {
+            const u32x4 w = q[i];
             f(nvrx_record{w.x, w.y});
             f(nvrx_record{w.z, w.w});
         }
     } else {
-        for (int64_t i = lo + lane; i < hi; i += 64) f(rs[i]);
+        int64_t i = lo + lane;
+        for (; i + 64 * (RB_UNROLL - 1) < hi; i += 64 * RB_UNROLL) {
+            nvrx_record w[RB_UNROLL];
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) w[u] = rs[i + 64 * u];
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) f(w[u]);
+        }
+        for (; i < hi; i += 64) f(rs[i]);
     }
 }
 
+template <int RB_WAVES>
 __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
@@ -161,16 +187,46 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     if (nstreams <= 0 || nslots <= 0) return hipSuccess;
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set && lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+    // Streams resident at once = blocks per CU x CUs.  One block per CU keeps the resident
+    // streams (read twice) and their bucket outputs (scattered 4-B writes) inside the
+    // 256 MB Infinity Cache: the second pass then reads from it and partial lines merge
+    // there instead of in HBM (configs[3] on MI355X: 5.6 ms with 6 blocks/CU -> 4.4 ms with
+    // one 4-wave block; 16-wave blocks contend on the shared LDS counters).
+    // NVRX_RB_WAVES (4 | 8 | 16) and NVRX_RB_BPC (blocks per CU, 0 = as many as fit) select
+    // the shape for A/B; LDS padding enforces the per-CU limit.
+    static const int waves = [] {
+        const char* e = getenv("NVRX_RB_WAVES");
+        const int w = e ? atoi(e) : 4;
+        return (w == 8 || w == 16) ? w : 4;
+    }();
+    static const int bpc = [] {
+        const char* e = getenv("NVRX_RB_BPC");
+        return e ? atoi(e) : 1;
+    }();
+    size_t lds_launch = lds;
+    if (bpc > 0) lds_launch = std::max(lds, (size_t)(160 * 1024) / (size_t)bpc - 1024);
+    if (lds_launch > NVRX_RECORDS_MAX_LDS) lds_launch = std::max(lds, (size_t)NVRX_RECORDS_MAX_LDS);
+    const void* fn = waves == 4    ? (const void*)records_bucket_kernel<4>
+                     : waves == 8 ? (const void*)records_bucket_kernel<8>
+                                  : (const void*)records_bucket_kernel<16>;
+    static bool attr_set[3] = {false, false, false};
+    const int wi = waves == 4 ? 0 : waves == 8 ? 1 : 2;
+    if (!attr_set[wi]) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            NVRX_RECORDS_MAX_LDS);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_set[wi] = true;
     }
-    hipLaunchKernelGGL(records_bucket_kernel, dim3((unsigned)nstreams), dim3(64 * RB_WAVES), lds, st, recs,
-                       rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts);
+    const dim3 grid((unsigned)nstreams), block(64 * waves);
+    if (waves == 4)
+        hipLaunchKernelGGL(records_bucket_kernel<4>, grid, block, lds_launch, st, recs, rec_off, nslots,
+                           cap, force_stable, seg_off, seg_len, out_ns, counts);
+    else if (waves == 8)
+        hipLaunchKernelGGL(records_bucket_kernel<8>, grid, block, lds_launch, st, recs, rec_off, nslots,
+                           cap, force_stable, seg_off, seg_len, out_ns, counts);
+    else
+        hipLaunchKernelGGL(records_bucket_kernel<16>, grid, block, lds_launch, st, recs, rec_off,
+                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts);
     return hipGetLastError();
 }
 

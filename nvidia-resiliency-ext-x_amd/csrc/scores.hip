@@ -46,13 +46,13 @@ __global__ __launch_bounds__(256) void kref_reduce_kernel(const int32_t* __restr
     const int64_t r1 = min(R, r0 + rows);
     uint32_t m = 0x7F800000u;
     bool miss = false;
-    for (int64_t r = r0; r < r1; ++r) {
+#pragma unroll 8
+    for (int64_t r = r0; r < r1; ++r) {  // unrolled: 8 independent loads in flight per thread
         const int64_t e = r * K + k;
-        if (num[e] <= 0) {
-            miss = true;
-        } else {
-            m = min(m, __float_as_uint(med[e]));
-        }
+        const int32_t c = num[e];
+        const uint32_t b = __float_as_uint(med[e]);
+        miss |= c <= 0;
+        m = c > 0 ? min(m, b) : m;
     }
     if (miss) atomicOr(&missing[k], 1u);
     atomicMin(&minbits[k], m);
@@ -72,8 +72,8 @@ hipError_t kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K
     const unsigned kb = (unsigned)((K + 255) / 256);
     hipLaunchKernelGGL(kref_init_kernel, dim3(kb), dim3(256), 0, st, minbits, missing, K);
     if (R > 0) {
-        // ~64 rows per thread keeps every load independent and the grid >> 256 CUs at scale
-        const int64_t rows = 64;
+        // 32 rows per thread: R/32 atomics per column, grid >> 256 CUs at scale
+        const int64_t rows = 32;
         const unsigned rb = (unsigned)((R + rows - 1) / rows);
         hipLaunchKernelGGL(kref_reduce_kernel, dim3(kb, rb), dim3(256), 0, st, num, med, R, K,
                            rows, minbits, missing);

@@ -319,26 +319,26 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
     emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
 }
 
-// HBM -> VGPR: the segment p[0:n) into v (64*PL slots, see fast_body), 16-byte buffer
-// loads from the 16-B aligned base below p.  m0 = p's offset in that 16-B vector (in
-// samples); x0 = p[0].  !FULL: slots outside the segment are set to x0.
-template <int PL, bool FULL>
-__device__ __forceinline__ void load_segment(const uint32_t* p, int n, unsigned (&v)[PL], int& m0,
-                                             unsigned& x0) {
+// HBM -> VGPR in two steps, so a caller can issue the next segment's loads before it
+// reduces the current one.  issue_loads: the segment p[0:n) into v (64*PL slots, see
+// fast_body) with 16-byte buffer loads from the 16-B aligned base below p; the descriptor
+// is built from wave-uniform (readfirstlane'd) inputs so the loads issue back to back (no
+// waterfall); lanes past the segment fall outside the descriptor's range (the hardware
+// returns 0).  finish_loads (after the loads landed): m0 = p's offset in its 16-B vector
+// (in samples), x0 = sample 0 (lane 0's slot m0: no extra memory access); !FULL sets the
+// slots outside the segment to x0 (a sample: neutral for MIN/MAX).
+template <int PL>
+__device__ __forceinline__ void issue_loads(const uint32_t* p, int n, unsigned (&v)[PL]) {
     constexpr int NV = PL / 4;
     const int lane = lane_id();
-    // The descriptor is built from wave-uniform (readfirstlane'd) inputs so the loads
-    // issue back to back (no waterfall); lanes past the segment fall outside the
-    // descriptor's range (the hardware returns 0) and are masked below.
     const uintptr_t pa = (uintptr_t)p & ~(uintptr_t)15;
-    m0 = (int)(((uintptr_t)p & 15) >> 2);
+    const int m0 = (int)(((uintptr_t)p & 15) >> 2);
     const int nvec = (n + m0 + 3) >> 2;
     const unsigned pa_lo = __builtin_amdgcn_readfirstlane((unsigned)pa);
     const unsigned pa_hi = __builtin_amdgcn_readfirstlane((unsigned)(pa >> 32));
     const int nbytes = __builtin_amdgcn_readfirstlane(nvec * 16);
     void* const pbase = (void*)(((uint64_t)pa_hi << 32) | pa_lo);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(pbase, 0, nbytes, 0x00020000);
-    x0 = p[0];
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane * 16, j * 1024, NVRX_LOAD_AUX);
@@ -347,13 +347,29 @@ __device__ __forceinline__ void load_segment(const uint32_t* p, int n, unsigned 
         v[4 * j + 2] = q.z;
         v[4 * j + 3] = q.w;
     }
+}
+
+template <int PL, bool FULL>
+__device__ __forceinline__ void finish_loads(const uint32_t* p, int n, unsigned (&v)[PL], int& m0,
+                                             unsigned& x0) {
+    const int lane = lane_id();
+    m0 = FULL ? 0 : (int)(((uintptr_t)p & 15) >> 2);
+    const unsigned e0 = m0 == 0 ? v[0] : m0 == 1 ? v[1] : m0 == 2 ? v[2] : v[3];
+    x0 = __builtin_amdgcn_readlane(e0, 0);
     if (!FULL) {
 #pragma unroll
         for (int i = 0; i < PL; ++i) {
             const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
-            v[i] = (e < (unsigned)n) ? v[i] : x0;  // x0 is a sample: neutral for min/max
+            v[i] = (e < (unsigned)n) ? v[i] : x0;
         }
     }
+}
+
+template <int PL, bool FULL>
+__device__ __forceinline__ void load_segment(const uint32_t* p, int n, unsigned (&v)[PL], int& m0,
+                                             unsigned& x0) {
+    issue_loads<PL>(p, n, v);
+    finish_loads<PL, FULL>(p, n, v, m0, x0);
 }
 
 // FULL: the host guarantees every segment holds exactly 64*PL samples starting on a

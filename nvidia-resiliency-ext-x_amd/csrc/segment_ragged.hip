@@ -244,25 +244,86 @@ void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
 }
 
 // ---------------------------------------------------------------- wave / workgroup classes
+// One wave per segment over a class list.  Waves take chunks of CH consecutive list
+// entries (static round robin; CH shrinks when the class is small so every wave gets
+// work); lanes 0..CH-1 fetch the chunk's segment descriptors in one coalesced access, so
+// per segment the only dependent memory access is the data itself -- and for PL <= 16
+// (short segments, few registers) the next segment's loads are issued before the
+// current one is reduced.
 template <int PL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OccV<PL, false>::W)))
+struct ListPrefetch {
+    static constexpr bool on = PL <= 16;
+};
+template <int PL>
+struct ListOcc {  // the prefetch buffer costs PL more VGPRs
+    static constexpr int W = PL == 16 ? 6 : OccV<PL, false>::W;
+};
+constexpr int LIST_CHUNK = 16;
+
+template <int PL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ListOcc<PL>::W)))
 void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
                            nvrx_stats_soa out, ColRef cr) {
     constexpr int NB = Bins<PL>::NB;
     __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id();
     unsigned* hist = lds_hist + wave * NB;
     const uint32_t start = cls[0], cnt = cls[1];
-    for (uint32_t i = blockIdx.x * 4u + wave; i < cnt; i += gridDim.x * 4u) {
-        const int64_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)list[start + i]);
+    const uint32_t G = gridDim.x * 4u;
+    const uint32_t CH = max(1u, min((uint32_t)LIST_CHUNK, cnt / (4u * G)));
+    for (uint32_t c0 = (blockIdx.x * 4u + wave) * CH; c0 < cnt; c0 += G * CH) {
+        const int m = (int)min(CH, cnt - c0);
+        uint32_t sid = 0, plo = 0, phi = 0;
+        int nn = 0;
+        if (lane < m) {
+            sid = list[start + c0 + lane];
+            const uint32_t* p;
+            segs.get(sid, p, nn);
+            plo = (uint32_t)(uintptr_t)p;
+            phi = (uint32_t)((uintptr_t)p >> 32);
+        }
+        auto desc = [&](int j, int64_t& s, const uint32_t*& p, int& n) {
+            s = (uint32_t)__builtin_amdgcn_readlane((int)sid, j);
+            p = (const uint32_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)phi, j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)plo, j));
+            n = __builtin_amdgcn_readlane(nn, j);
+        };
+        int64_t s;
         const uint32_t* p;
         int n;
-        segs.get(s, p, n);
+        desc(0, s, p, n);
         unsigned v[PL];
-        int m0;
-        unsigned x0;
-        load_segment<PL, false>(p, n, v, m0, x0);
-        fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+        if (ListPrefetch<PL>::on) {
+            issue_loads<PL>(p, n, v);
+            for (int j = 0; j < m; ++j) {
+                // unconditional prefetch (the last one re-reads the current segment): a load
+                // under a branch would make the waitcnt at the join cover it
+                int64_t s2;
+                const uint32_t* p2;
+                int n2;
+                desc(j + 1 < m ? j + 1 : j, s2, p2, n2);
+                unsigned w[PL];
+                issue_loads<PL>(p2, n2, w);
+                int m0;
+                unsigned x0;
+                finish_loads<PL, false>(p, n, v, m0, x0);
+                fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+#pragma unroll
+                for (int i = 0; i < PL; ++i) v[i] = w[i];
+                s = s2;
+                p = p2;
+                n = n2;
+            }
+        } else {
+            for (int j = 0; j < m; ++j) {
+                if (j) desc(j, s, p, n);
+                int m0;
+                unsigned x0;
+                load_segment<PL, false>(p, n, v, m0, x0);
+                fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+            }
+        }
     }
 }
 
@@ -324,7 +385,7 @@ void launch_lane(const RaggedSegs& segs, const uint32_t* list, const uint32_t* c
 template <int PL>
 void launch_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
                  const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
-    const unsigned blocks = (unsigned)(cu_count() * OccV<PL, false>::W);
+    const unsigned blocks = (unsigned)(cu_count() * ListOcc<PL>::W);
     hipLaunchKernelGGL((seg_stats_list_kernel<PL>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
                        out, cr);
 }

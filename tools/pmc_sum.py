@@ -4,12 +4,18 @@ import csv
 import glob
 import sys
 
+def short(name):
+    base = name.replace("(anonymous namespace)::", "").split("(")[0]
+    base = base.replace("void ", "").replace("nvrx::", "")
+    return base[-42:]
+
+
 for d in sys.argv[1:]:
     agg = collections.defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "seg_" in r["Kernel_Name"]:
-                agg[(r["Kernel_Name"].split("(")[0][-40:], r["Counter_Name"])].append(float(r["Counter_Value"]))
+            if any(t in r["Kernel_Name"] for t in ("seg_", "records_", "classify")):
+                agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     waves = {k[0]: sum(v) / len(v) for k, v in agg.items() if k[1] == "SQ_WAVES"}
     for (kn, c), v in sorted(agg.items()):
         m = sum(v) / len(v)
