@@ -217,7 +217,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-ranks", type=int, default=16)
     ap.add_argument("--no-zipf", action="store_true")
-    ap.add_argument("--zipf-cpu-ranks", type=int, default=128)
+    ap.add_argument("--zipf-cpu-ranks", type=int, default=1024)
     args = ap.parse_args()
     rank, world, dev = dist_setup()
     if world != args.gpus:

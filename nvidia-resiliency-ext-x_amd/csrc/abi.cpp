@@ -184,7 +184,28 @@ int nvrx_stragglers(const double* score, int64_t n, double thr, uint8_t* mask, v
 int64_t nvrx_records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
     return nvrx::records_bucket_capacity(n, nstreams, nslots);
 }
-int64_t nvrx_records_max_slots(void) { return NVRX_RECORDS_MAX_LDS / (3 * sizeof(uint32_t)); }
+int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                       int64_t nslots, int64_t cap, int32_t mode, int64_t max_len, int64_t* seg_off,
+                       int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
+                       const nvrx_stats_soa* out, uint32_t* col_ref, void* stream) {
+    NVRX_CHECK_ARG(nstreams >= 0 && nslots >= 0 && max_len >= 0, "nvrx_records_stats: negative size");
+    NVRX_CHECK_ARG(nslots <= nvrx_records_max_slots(), "nvrx_records_stats: too many slots");
+    NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
+                   "nvrx_records_stats: null output array");
+    NVRX_CHECK_ARG(nstreams == 0 || nslots == 0 ||
+                       (recs && rec_off && seg_off && seg_len && out_ns && counts),
+                   "nvrx_records_stats: null array");
+    NVRX_CHECK_ARG(mode == NVRX_STATS_FAST || mode == NVRX_STATS_EXACT,
+                   "nvrx_records_stats: unknown mode");
+    NVRX_CHECK_ARG(nstreams * nslots < (int64_t)1 << 31, "nvrx_records_stats: too many segments");
+    const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
+    NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT, "nvrx_records_stats: retained run longer than NVRX_MAX_SEGMENT");
+    return hip_status(nvrx::records_stats(recs, rec_off, nstreams, nslots, cap, mode, max_len,
+                                          seg_off, seg_len, out_ns, counts, *out, col_ref, S(stream)),
+                      "nvrx_records_stats");
+}
+
+int64_t nvrx_records_max_slots(void) { return NVRX_RECORDS_MAX_LDS / (3 * sizeof(uint32_t)); }  // W = 1
 
 int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                         int64_t nslots, int64_t cap, int64_t* seg_off, int32_t* seg_len,

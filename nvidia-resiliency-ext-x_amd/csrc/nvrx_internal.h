@@ -38,6 +38,10 @@ int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots);
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
                           int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st);
+hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                         int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
+                         int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
+                         const nvrx_stats_soa& out, uint32_t* col_ref, hipStream_t st);
 hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, const int64_t* dst_off,
                             const uint32_t* ns, int64_t nslots, nvrx_record* out, hipStream_t st);
 

@@ -78,7 +78,8 @@ hipError_t kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K
         hipLaunchKernelGGL(kref_reduce_kernel, dim3(kb, rb), dim3(256), 0, st, num, med, R, K,
                            rows, minbits, missing);
     }
-    hipLaunchKernelGGL(kref_final_kernel, dim3(kb), dim3(256), 0, st, minbits, missing, K, R, ref);
+    if (ref)  // NULL: the caller consumes the [minbits | missing] words of `scratch`
+        hipLaunchKernelGGL(kref_final_kernel, dim3(kb), dim3(256), 0, st, minbits, missing, K, R, ref);
     return hipGetLastError();
 }
 

@@ -19,7 +19,8 @@ struct StridedSegs {  // segment s = base[s*stride + begin : + len], last `cap` 
         n = (int)keep;
     }
 };
-struct RaggedSegs {  // segment s = base[off[s] : off[s] + len[s]] (len NULL: off[s+1]), last `cap` kept
+struct RaggedSegs {  // segment s = base[off[s] : off[s] + len[s]] (len NULL: off[s+1]), last `cap` kept;
+                     // len[s] < 0: skipped (already reduced, e.g. by records_stats)
     const uint32_t* base;
     const int64_t* off;
     const int32_t* lens;
@@ -389,8 +390,8 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     const uint32_t* p;
     int n;
     segs.get(s, p, n);
-    if (n <= 0) {
-        if (lane == 0) {
+    if (n <= 0) {  // n < 0: segment reduced elsewhere (records_stats), outputs untouched
+        if (n == 0 && lane == 0) {
             write_empty(out, s);
             cr.miss(s);
         }
@@ -402,6 +403,67 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     unsigned x0;
     load_segment<PL, FULL>(p, n, v, m0, x0);
     fast_body<PL, FULL>(v, n, m0, x0, s, hist, out, cr);
+}
+
+// Ascending bitonic sorting network over N registers (N a power of two): compile-time
+// compare-exchanges, i.e. v_min/v_max pairs -- no LDS, no branches.
+template <int N>
+__device__ __forceinline__ void sort_net(unsigned (&v)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned a = v[i], b = v[l];
+                    const bool up = (i & k) == 0;
+                    v[i] = up ? min(a, b) : max(a, b);
+                    v[l] = up ? max(a, b) : min(a, b);
+                }
+            }
+        }
+    }
+}
+
+// One segment of 1..N samples per LANE (v: the n samples in any order, slots >= n
+// ignored).  u32 -> f32 us is monotone, so sorting the integer ns sorts the floats
+// computeStats sorts; then CuptiProfiler.cpp:53-71 statement by statement (sequential f32
+// sums over the sorted samples) -- every field bit-exact.
+template <int N>
+__device__ __forceinline__ void lane_stats(unsigned (&v)[N], int n, int64_t s,
+                                           const nvrx_stats_soa& out, const ColRef& cr) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[j] = j < n ? v[j] : 0xFFFFFFFFu;  // sentinels sort last
+    sort_net<N>(v);
+    const int i0 = (n & 1) ? n / 2 : n / 2 - 1, i1 = n / 2;
+    float fmin = 0.0f, fmax = 0.0f, f0 = 0.0f, f1 = 0.0f, acc = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const float f = ns_to_us(v[j]);
+        v[j] = __float_as_uint(f);
+        if (j == 0) fmin = f;
+        if (j == n - 1) fmax = f;
+        if (j == i0) f0 = f;
+        if (j == i1) f1 = f;
+        acc = j < n ? acc + f : acc;  // accumulate(sorted, 0.0f): sequential f32
+    }
+    const float med = (n & 1) ? f0 : (f0 + f1) / 2;
+    const float avg = acc / (float)n;
+    float sq = 0.0f;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const float t = __uint_as_float(v[j]) - avg;
+        sq = j < n ? sq + t * t : sq;
+    }
+    out.num[s] = n;
+    out.min[s] = fmin;
+    out.max[s] = fmax;
+    out.med[s] = med;
+    out.avg[s] = avg;
+    out.std[s] = (float)__builtin_sqrt((double)(sq / (float)n));  // sqrtf, correctly rounded
+    cr.add(s, med);
 }
 
 // ---------------------------------------------------------------------------
@@ -472,8 +534,8 @@ __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t
     const uint32_t* p;
     int n;
     segs.get(s, p, n);
-    if (n <= 0) {
-        if (threadIdx.x == 0) {
+    if (n <= 0) {  // n < 0: reduced elsewhere
+        if (n == 0 && threadIdx.x == 0) {
             write_empty(out, s);
             cr.miss(s);
         }

@@ -87,10 +87,10 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
             const uint32_t* p;
             int n;
             segs.get(s, p, n);
-            if (n <= 0) {
+            if (n == 0) {
                 write_empty(out, s);
                 cr.miss(s);
-            } else {
+            } else if (n > 0) {  // n < 0: reduced elsewhere
                 cls = seg_class(n, aligned16 != 0, exact != 0);
             }
         }
@@ -155,28 +155,6 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
 }
 
 // ---------------------------------------------------------------- lane classes
-// Ascending bitonic sorting network over N registers (N a power of two): compile-time
-// compare-exchanges, i.e. v_min/v_max pairs -- no LDS, no branches.
-template <int N>
-__device__ __forceinline__ void sort_net(unsigned (&v)[N]) {
-#pragma unroll
-    for (int k = 2; k <= N; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const unsigned a = v[i], b = v[l];
-                    const bool up = (i & k) == 0;
-                    v[i] = up ? min(a, b) : max(a, b);
-                    v[l] = up ? max(a, b) : min(a, b);
-                }
-            }
-        }
-    }
-}
-
 template <int N>
 struct LaneOcc {
     static constexpr int W = N >= 64 ? 4 : N >= 32 ? 6 : 8;
@@ -210,36 +188,7 @@ void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
 #pragma unroll
             for (int j = 0; j < N; ++j) v[j] = j < n ? p[j] : 0xFFFFFFFFu;
         }
-#pragma unroll
-        for (int j = 0; j < N; ++j) v[j] = j < n ? v[j] : 0xFFFFFFFFu;  // sentinels sort last
-        sort_net<N>(v);
-        const int i0 = (n & 1) ? n / 2 : n / 2 - 1, i1 = n / 2;
-        float fmin = 0.0f, fmax = 0.0f, f0 = 0.0f, f1 = 0.0f, acc = 0.0f;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const float f = ns_to_us(v[j]);
-            v[j] = __float_as_uint(f);
-            if (j == 0) fmin = f;
-            if (j == n - 1) fmax = f;
-            if (j == i0) f0 = f;
-            if (j == i1) f1 = f;
-            acc = j < n ? acc + f : acc;  // accumulate(sorted, 0.0f): sequential f32
-        }
-        const float med = (n & 1) ? f0 : (f0 + f1) / 2;
-        const float avg = acc / (float)n;
-        float sq = 0.0f;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const float t = __uint_as_float(v[j]) - avg;
-            sq = j < n ? sq + t * t : sq;
-        }
-        out.num[s] = n;
-        out.min[s] = fmin;
-        out.max[s] = fmax;
-        out.med[s] = med;
-        out.avg[s] = avg;
-        out.std[s] = (float)__builtin_sqrt((double)(sq / (float)n));  // sqrtf, correctly rounded
-        cr.add(s, med);
+        lane_stats<N>(v, n, s, out, cr);
     }
 }
 
@@ -410,9 +359,6 @@ hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const
 
 }  // namespace
 
-// Below this many segments the one-shot launch (one wave per segment, PL sized for
-// max_len) is cheaper than classifying.
-constexpr int64_t RAGGED_CLASSIFY_MIN = 4096;
 
 hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
                                 int64_t nseg, int64_t max_len, int64_t cap, int mode,
@@ -426,10 +372,6 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
     const int64_t need = aligned16 ? keep : keep + 3;
     const bool exact = mode == NVRX_STATS_EXACT;
-    if (nseg < RAGGED_CLASSIFY_MIN) {
-        if (exact || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
-        return launch_fast(segs, nseg, need, -1, out, cr, st);  // lengths vary: masked variant
-    }
     if (nseg >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
 
     const int64_t nblocks = std::min<int64_t>(CLS_MAX_BLOCKS, (nseg + CLS_THREADS - 1) / CLS_THREADS);

@@ -80,6 +80,8 @@ SIGNATURES = {
     "nvrx_stragglers": (ctypes.c_int, [P, i64, f64, P, P]),
     "nvrx_section_stats": (ctypes.c_int, [P, P, i64, i64, P, P, P, P, P, P, P]),
     "nvrx_records_bucket_capacity": (i64, [i64, i64, i64]),
+    "nvrx_records_stats": (ctypes.c_int, [P, P, i64, i64, i64, i32, i64, P, P, P, P,
+                                          ctypes.POINTER(StatsSoA), P, P]),
     "nvrx_records_bucket": (ctypes.c_int, [P, P, i64, i64, i64, P, P, P, P, P]),
     "nvrx_records_max_slots": (i64, []),
     "nvrx_profiler_create": (ctypes.c_int, [ctypes.POINTER(ProfilerConfig), ctypes.POINTER(P)]),

@@ -117,14 +117,10 @@ class MatrixReporter:
                  torch.empty(max(need, 1), dtype=torch.int32, device=d),
                  torch.empty(self.R * self.K, dtype=torch.int32, device=d))
             self._bucket = b
-        seg_off, seg_len, out_ns, _ = ops.records_bucket(recs, rec_off, self.K, self.cap, out=b)
         max_len = min(self.cap, n) if self.cap > 0 else n
-        st = ops.segment_stats_ragged(out_ns, seg_off, seg_len, max_len=max(max_len, 1), cap=0,
-                                      mode=self.mode, aligned16=True, out=self.stats,
-                                      col_ref=self.col_ref if self._fuse_ref() else None,
-                                      ncols=self.K)
-        self._column_ref()
-        return st
+        return ops.records_stats(recs, rec_off, self.K, self.cap, max(max_len, 1), mode=self.mode,
+                                 out=self.stats, bucket=b,
+                                 col_ref=self.col_ref if self.relative else None)
 
     def report_records(self, recs: torch.Tensor, rec_off: torch.Tensor) -> BatchResult:
         """One full report from record streams resident in HBM."""

@@ -214,3 +214,31 @@ def records_bucket(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: 
            seg_off.data_ptr(), seg_len.data_ptr(), out_ns.data_ptr(), counts.data_ptr(),
            _stream(stream))
     return seg_off, seg_len, out_ns, counts
+
+
+def records_stats(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: int, max_len: int,
+                  mode: int = STATS_FAST, out: Optional[SegmentStats] = None, bucket=None,
+                  col_ref: Optional[torch.Tensor] = None, stream=None) -> SegmentStats:
+    """Per-(stream, slot) statistics of push-ordered record streams (ring retention of the
+    last `cap` + computeStats): bucketing, then the length-classed segment kernels.  `bucket` may pass the
+    (seg_off, seg_len, out_ns, counts) work tensors preallocated; col_ref ([2*nslots] int32)
+    receives the per-slot reference (min over streams of MED | missing)."""
+    nstreams = rec_off.numel() - 1
+    dev = recs.device
+    n = recs.shape[0]
+    cap_ns = records_bucket_capacity(n, nstreams, nslots)
+    if bucket is None:
+        bucket = (torch.empty(nstreams * nslots, dtype=torch.int64, device=dev),
+                  torch.empty(nstreams * nslots, dtype=torch.int32, device=dev),
+                  torch.empty(max(cap_ns, 1), dtype=torch.int32, device=dev),
+                  torch.empty(nstreams * nslots, dtype=torch.int32, device=dev))
+    seg_off, seg_len, out_ns, counts = bucket
+    if out_ns.numel() < cap_ns or seg_off.numel() < nstreams * nslots:
+        raise ValueError("records_stats: preallocated work tensors too small")
+    if out is None:
+        out = SegmentStats.empty(nstreams * nslots, dev)
+    soa = out.soa()
+    N.call("nvrx_records_stats", recs.data_ptr(), rec_off.data_ptr(), nstreams, nslots, cap, mode,
+           max_len, seg_off.data_ptr(), seg_len.data_ptr(), out_ns.data_ptr(), counts.data_ptr(),
+           ctypes.byref(soa), N.ptr(col_ref), _stream(stream))
+    return out

@@ -174,3 +174,39 @@ def test_cupti_manager_refcount():
         assert m.get_results() == {}
     finally:
         m.shutdown()
+
+
+@pytest.mark.parametrize("nslots,cap,lo,hi", [(37, 8192, 0, 40), (37, 5, 0, 30), (3000, 0, 0, 3),
+                                              (500, 100, 0, 150), (64, 8192, 60, 70)])
+def test_records_stats_fused_matches_oracle(nslots, cap, lo, hi):
+    # short retained runs reduced inside the bucketing workgroup, the rest by the ragged
+    # kernels: every field vs the oracle's ring-push + computeStats restatement
+    rng = np.random.default_rng(nslots + cap + hi)
+    nstreams = 6
+    recs, off = _streams(rng, nstreams, nslots, lo, hi)
+    # an empty stream in the middle
+    recs = np.concatenate([recs[:off[2]], recs[off[3]:]])
+    off = np.concatenate([off[:3], off[3:] - (off[3] - off[2])])
+    off = np.concatenate([off[:3], [off[2]], off[3:]])[:nstreams + 1]
+    recs = recs[:off[-1]]
+    d_recs = torch.from_numpy(np.ascontiguousarray(recs).view(np.int32)).cuda()
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    max_len = int(np.diff(off).max())
+    col = torch.empty(2 * nslots, dtype=torch.int32, device="cuda")
+    st = ops.records_stats(d_recs, d_off, nslots, cap, max(1, min(max_len, cap) if cap else max_len),
+                           mode=ops.STATS_FAST, col_ref=col).cpu()
+    ref = O.records_stats(recs, off.astype(np.int64), nslots, cap=cap, nthreads=4)
+    for f in ("num", "min", "max", "med"):
+        assert np.array_equal(getattr(st, f).numpy().view(np.int32), ref[f].view(np.int32)), f
+    short = (ref["num"] > 0) & (ref["num"] <= 64)
+    for f in ("avg", "std"):
+        a = getattr(st, f).numpy()
+        assert np.array_equal(a[short].view(np.int32), ref[f][short].view(np.int32)), f
+        both = ref["num"] > 0
+        np.testing.assert_allclose(a[both], ref[f][both], rtol=1e-4)
+    num = ref["num"].reshape(nstreams, nslots)
+    want = O.kernel_ref(num, ref["med"].reshape(nstreams, nslots))
+    c = col.cpu().numpy()
+    miss = c[nslots:] != 0
+    assert np.array_equal(miss, (num == 0).any(axis=0))
+    assert np.array_equal(c[:nslots].view(np.float32)[~miss], want[~miss])

@@ -28,11 +28,10 @@ for _ in range(n):
     e[0].record()
     ops.records_bucket(recs, rec_off, K, CAP, out=b)
     e[1].record()
-    ops.segment_stats_ragged(b[2], b[0], b[1], max_len=CAP, cap=0, aligned16=True, out=rep.stats)
-    rep._column_ref()
+    rep.compute_stats_records(recs, rec_off)  # fused path (bucket + in-block short runs + rest)
     e[2].record()
     torch.cuda.synchronize()
     tb += e[0].elapsed_time(e[1])
     ts += e[1].elapsed_time(e[2])
 print(f"R={R} records={R*N} bucket_ms={tb/n:.3f} ({R*N*16/(tb/n)/1e6:.0f} GB/s at 16 B/rec) "
-      f"stats_ms={ts/n:.3f}")
+      f"fused_records_stats_ms={ts/n:.3f}")
