@@ -1,0 +1,89 @@
+"""CPU: host-side logic of the scoring path that involves no device -- the report interval
+tracker (reference tests/straggler/unit/test_interval_tracker.py), name-id agreement across
+ranks (name_mapper.py:56-81) and the dist_utils collectives, on gloo worlds."""
+import time
+
+import pytest
+
+from _mp import run_world
+
+
+def test_interval_estimate_single_process():
+    from nvidia_resiliency_ext.straggler import interval_tracker
+
+    tr = interval_tracker.ReportIntervalTracker()
+    tr.time_interval = 0.5
+    assert tr.iter_interval is None
+    for i in range(120):
+        tr.iter_increase()
+        time.sleep(0.01)
+        if tr.current_iter <= tr.INTERVAL_ESTIMATION_ITERS:
+            assert tr.iter_interval is None
+        else:
+            assert tr.is_interval_elapsed() == (tr.current_iter % tr.iter_interval == 0)
+        if i < tr.INTERVAL_ESTIMATION_ITERS // 2:
+            time.sleep(0.04)  # slow warm-up steps do not move the (lower) median
+    assert not tr.step_times
+    assert abs(tr.iter_interval - 50) < 5
+
+
+def test_interval_never_below_profiling_interval():
+    from nvidia_resiliency_ext.straggler.interval_tracker import ReportIntervalTracker
+
+    tr = ReportIntervalTracker(time_interval=1e-6, profiling_interval=7)
+    for _ in range(tr.INTERVAL_ESTIMATION_ITERS + 1):
+        tr.iter_increase()
+    assert tr.iter_interval == 7
+    with pytest.raises(AssertionError):
+        tr._gather_report_interval()
+
+
+def test_interval_is_max_over_ranks():
+    # rank 1 steps 4x faster -> more iterations per interval; every rank takes the MAX
+    res = run_world(2, "_host_workers", "interval_world", step_s=[0.02, 0.005])
+    assert res[0] == res[1]
+    assert 40 <= res[0] <= 90
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_name_ids_agree_across_ranks(ws):
+    res = run_world(ws, "_host_workers", "name_mapper_world")
+    ref = res[0]
+    for r in range(ws):
+        assert res[r] == ref
+    kid, sid = ref["r1"]
+    # gathered order: rank by rank, list order
+    want = {}
+    for r in range(ws):
+        for n in (f"k_rank{r}", "shared"):
+            want.setdefault(n, len(want))
+    assert kid == want and sid == {"sec": 0}
+    assert ref["r2"] == kid
+    kid3, sid3 = ref["r3"]
+    assert kid3 == {**want, "late_b": len(want), "late_a": len(want) + 1}
+    assert sid3 == {"sec": 0, "sec2": 1}
+
+
+def test_dist_utils_on_gloo():
+    res = run_world(3, "_host_workers", "dist_utils_world")
+    for r in range(3):
+        o = res[r]
+        assert (o["ws"], o["rank"], o["dev"]) == (3, r, "cpu")
+        assert o["all_true"] is True and o["one_false"] is False
+        assert o["objs"] == [{"r": 0}, {"r": 1}, {"r": 2}]
+        assert o["sum"] == 6.0
+    assert res[0]["gather"] == [[0.0, 0.0], [1.0, 10.0], [2.0, 20.0]]
+    assert res[1]["gather"] is None and res[2]["gather"] is None
+
+
+def test_dist_utils_single_process_is_local():
+    import torch
+
+    from nvidia_resiliency_ext.straggler import dist_utils as du
+
+    assert du.get_world_size() == 1 and du.get_rank() == 0
+    t = torch.tensor([3.0])
+    du.all_reduce(t)
+    assert t.item() == 3.0
+    assert du.gather_on_rank0(t)[0] is t
+    assert du.is_all_true(False) is False and du.all_gather_object(5) == [5]
