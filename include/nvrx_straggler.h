@@ -230,6 +230,12 @@ int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, u
                             int32_t* num, float* mn, float* mx, float* med, float* avg,
                             float* sd);
 int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_t buflen);
+/* Flush, then copy the record log since the last reset ({slot, ns}, push order per slot;
+ * after a compaction only the records the rings can still retain) into host `out`
+ * (up to cap_out records; *count = log length).  Synchronous.  No reference counterpart:
+ * it lets a caller (the live-capture parity check) recompute the statistics elsewhere. */
+int nvrx_profiler_get_records(nvrx_profiler* p, int64_t cap_out, int64_t* count,
+                              nvrx_record* out);
 /* Live kernel-dispatch capture through rocprofiler-sdk (CuptiProfiler.cpp:96-203).
  * nvrx_capture_configure registers the library as a rocprofiler-sdk tool; it must run
  * before the process's first HIP call (NVRX_ERR_STATE otherwise).  Once the runtime has
@@ -239,6 +245,9 @@ int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_
  * integer-ns duration; nvrx_profiler_stop / _get_stats flush the capture buffer first. */
 int nvrx_capture_configure(void);
 int nvrx_profiler_capture_available(void);
+/* Deliver the dispatch records completed so far to the started / stopped profiler
+ * (cuptiActivityFlushAll(0), CuptiProfiler.cpp:138).  Synchronous; no-op without capture. */
+int nvrx_capture_flush(void);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -400,9 +400,13 @@ int flush_locked(nvrx_profiler* p) {
 
 namespace nvrx {
 // capture.cpp's dispatch callback: one completed kernel under its composite key
+// The dispatch context only produces records for kernels enqueued while it was started;
+// such a kernel may complete (and its record arrive) after stop, and is still counted, as
+// CUPTI delivers the activity records of kernels launched while the activity kind was
+// enabled (bufferCompleted, CuptiProfiler.cpp:168-203, pushes regardless of _isStarted).
 void profiler_push_named(nvrx_profiler* p, const char* key, uint32_t ns) {
     std::lock_guard<std::mutex> lk(p->mu);
-    if (!p->started) return;
+    if (!p->initialized) return;
     auto it = p->name_to_slot.find(key);
     uint32_t slot;
     if (it != p->name_to_slot.end()) {
@@ -506,6 +510,7 @@ int nvrx_profiler_stop(nvrx_profiler* p) {
 
 int nvrx_profiler_reset(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_reset: null handle");
+    (void)nvrx::capture_flush();  // CuptiProfiler.cpp:149: flush, then clear (outside the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     p->staged.clear();  // CuptiProfiler.cpp:148-152: flush + clear all rings
     p->log_n = 0;
@@ -594,6 +599,24 @@ int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, u
         if (sd) sd[i] = hsd[s];
     }
     return NVRX_OK;
+}
+
+int nvrx_profiler_get_records(nvrx_profiler* p, int64_t cap_out, int64_t* count,
+                              nvrx_record* out) {
+    NVRX_CHECK_ARG(p && count && cap_out >= 0 && (cap_out == 0 || out),
+                   "nvrx_profiler_get_records: bad arguments");
+    (void)nvrx::capture_flush();
+    std::lock_guard<std::mutex> lk(p->mu);
+    DeviceGuard g(p->cfg.device);
+    int rc = flush_locked(p);
+    if (rc) return rc;
+    *count = p->log_n;
+    const int64_t m = std::min<int64_t>(cap_out, p->log_n);
+    if (m == 0) return NVRX_OK;
+    hipError_t e = hipMemcpyAsync(out, p->d_log, (size_t)m * sizeof(nvrx_record),
+                                  hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    return hip_status(e, "nvrx_profiler_get_records: download");
 }
 
 int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_t buflen) {

@@ -21,6 +21,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -39,6 +40,9 @@ struct Capture {
     std::atomic<bool> ready{false};      // tool_init completed
     std::atomic<bool> requested{false};  // nvrx_capture_configure succeeded
     std::atomic<nvrx_profiler*> target{nullptr};
+    // diagnostics of the capture's cost (tools/live_gpt2.py):
+    bool discard = false;       // NVRX_CAPTURE_DISCARD=1: drop records (the tracer alone)
+    bool keep_started = false;  // NVRX_CAPTURE_KEEP_STARTED=1: never stop the dispatch context
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -65,7 +69,7 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
                         rocprofiler_record_header_t** headers, size_t num_headers, void*,
                         uint64_t) {
     nvrx_profiler* p = cap().target.load();
-    if (!p) return;
+    if (!p || cap().discard) return;
     char key[4096];
     for (size_t i = 0; i < num_headers; ++i) {
         const rocprofiler_record_header_t* h = headers[i];
@@ -95,6 +99,10 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
     Capture& c = cap();
+    const char* d = std::getenv("NVRX_CAPTURE_DISCARD");
+    c.discard = d && d[0] == '1';
+    const char* k = std::getenv("NVRX_CAPTURE_KEEP_STARTED");
+    c.keep_started = k && k[0] == '1';
     if (rocprofiler_create_context(&c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
     if (rocprofiler_configure_callback_tracing_service(c.sym_ctx,
                                                        ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT,
@@ -102,7 +110,9 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
                                                        nullptr) != ROCPROFILER_STATUS_SUCCESS)
         return -1;
     if (rocprofiler_create_context(&c.disp_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
-    if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, 6u << 20, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
+    size_t watermark = 1u << 20;  // ~ the Detector's CUPTI bufferSize (1 MB, cupti.py:25)
+    if (const char* w = std::getenv("NVRX_CAPTURE_WATERMARK")) watermark = std::strtoull(w, nullptr, 10);
+    if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, watermark, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
                                   dispatch_buffer_cb, nullptr, &c.buffer) != ROCPROFILER_STATUS_SUCCESS)
         return -1;
     if (rocprofiler_configure_buffer_tracing_service(c.disp_ctx,
@@ -145,11 +155,11 @@ int capture_start(nvrx_profiler* p) {
 
 int capture_stop(nvrx_profiler* p) {
     Capture& c = cap();
-    if (!c.ready) return 0;
-    int rc = rocprofiler_stop_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
-    (void)rocprofiler_flush_buffer(c.buffer);  // deliver what completed while started
+    if (!c.ready || c.keep_started) return 0;
+    // no flush here: records of kernels enqueued while started are delivered later (buffer
+    // watermark, get_stats / reset flush) and still counted, as CUPTI's are
     (void)p;
-    return rc;
+    return rocprofiler_stop_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
 }
 
 int capture_flush() {
@@ -184,5 +194,13 @@ int nvrx_capture_configure(void) {
 }
 
 int nvrx_profiler_capture_available(void) { return cap().ready.load() ? 1 : 0; }
+
+int nvrx_capture_flush(void) {
+    if (nvrx::capture_flush() != 0) {
+        nvrx::set_error("nvrx_capture_flush: rocprofiler_flush_buffer failed");
+        return NVRX_ERR_RUNTIME;
+    }
+    return NVRX_OK;
+}
 
 }  // extern "C"

@@ -95,7 +95,9 @@ SIGNATURES = {
     "nvrx_profiler_push": (ctypes.c_int, [P, P, i64]),
     "nvrx_profiler_get_stats": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P, P, P, P, P, P, P]),
     "nvrx_profiler_kernel_name": (ctypes.c_int, [P, u32, ctypes.c_char_p, i64]),
+    "nvrx_profiler_get_records": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P]),
     "nvrx_profiler_capture_available": (ctypes.c_int, []),
+    "nvrx_capture_flush": (ctypes.c_int, []),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -155,6 +155,24 @@ class KernelProfiler:
         names = [self._name_of(int(s)) for s in slots]
         return KernelSummaries(names, num, *cols)
 
+    def get_records(self):
+        """(slots u32, ns u32) of the device record log since the last reset, push order
+        (nvrx_profiler_get_records) -- what the statistics are computed from."""
+        count = ctypes.c_int64()
+        N.call("nvrx_profiler_get_records", self._h, 0, ctypes.byref(count), None)
+        recs = np.empty((int(count.value), 2), np.uint32)
+        N.call("nvrx_profiler_get_records", self._h, len(recs), ctypes.byref(count),
+               recs.ctypes.data)
+        return recs[:, 0].copy(), recs[:, 1].copy()
+
+    def flush_capture(self):
+        """Deliver completed dispatch records now (cuptiActivityFlushAll)."""
+        N.call("nvrx_capture_flush")
+
+    def name_of(self, slot: int) -> str:
+        """Composite kernel name of a record slot."""
+        return self._name_of(int(slot))
+
     def _name_of(self, s: int) -> str:
         """Slot -> composite name; slots created by the capture callback are fetched once."""
         if s < len(self._names) and self._names[s] is not None:

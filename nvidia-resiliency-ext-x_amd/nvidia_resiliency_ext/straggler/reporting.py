@@ -104,7 +104,7 @@ class _History:
                 self.names.append(n)
         need = len(self.names)
         cap = 0 if self.values is None else self.values.numel()
-        if need > cap:
+        if need > cap or self.values is None:  # allocated on first use, even with no names
             new = torch.full((max(need, 2 * cap, 64),), float("inf"), dtype=torch.float64,
                              device=device)
             if self.values is not None:

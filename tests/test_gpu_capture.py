@@ -71,3 +71,43 @@ def test_dispatch_capture_ring_cap():
     out = _run(cap=4, nstrag=9)
     strag = [v for k, v in out["stats"].items() if "stragglers" in k]
     assert strag and strag[0][0] == 4
+
+
+ASYNC_CHILD = r"""
+import json, sys
+sys.path.insert(0, %(pkg)r)
+from nvidia_resiliency_ext.straggler import cupti, ops
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=1024, capture=True)
+p.initialize()
+x = torch.randn(4096, 4096, device="cuda")
+score = torch.rand(1000, dtype=torch.float64, device="cuda")
+torch.cuda.synchronize()
+p.start()
+for _ in range(40):
+    y = x @ x                 # keeps the queue busy well past stop()
+for _ in range(7):
+    ops.stragglers(score, 0.5)
+p.stop()                      # no synchronize: the 7 launches have not run yet
+pending = not torch.cuda.current_stream().query()
+torch.cuda.synchronize()
+st = p.get_stats()
+out = {"pending_at_stop": pending,
+       "strag": sum(v.num_calls for k, v in st.items() if "stragglers" in k)}
+p.reset()
+for _ in range(5):
+    ops.stragglers(score, 0.5)  # stopped: not captured
+torch.cuda.synchronize()
+out["after_reset"] = len(p.get_stats())
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_dispatch_completing_after_stop_is_captured():
+    code = ASYNC_CHILD % dict(pkg=os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][7:])
+    assert out["pending_at_stop"]
+    assert out["strag"] == 7      # enqueued while started, completed after stop
+    assert out["after_reset"] == 0

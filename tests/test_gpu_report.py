@@ -64,6 +64,23 @@ def test_individual_one_rank_history():
     assert rep({'kernel0': get_summary(a), 'kernel1': get_summary(b)}) == pytest.approx(0.5)
 
 
+@pytest.mark.parametrize("gather", [False, True])
+def test_first_report_sections_only(gather):
+    # no kernel captured yet (e.g. sections timed with profile_cuda=False): the GPU scores
+    # are NaN (reporting.py:237-253, empty kernel summaries), the section scores are 1.0
+    from nvidia_resiliency_ext import straggler
+    from _report_workers import get_summary
+
+    rg = straggler.reporting.ReportGenerator(['relative_perf_scores', 'individual_perf_scores'],
+                                             gather_on_rank0=gather, node_name='testnode')
+    for _ in range(2):
+        r = rg.generate_report({'step': get_summary(np.array([3.0, 4.0, 5.0]))}, {})
+        assert math.isnan(r.gpu_relative_perf_scores[0])
+        assert math.isnan(r.gpu_individual_perf_scores[0])
+        assert r.section_relative_perf_scores['step'][0] == pytest.approx(1.0)
+        assert r.section_individual_perf_scores['step'][0] == pytest.approx(1.0)
+
+
 def test_name_mapper_single_rank():
     # test_name_mapper.py:48-123
     from nvidia_resiliency_ext import straggler
