@@ -306,7 +306,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic,
-                         "kernel": "seg_stats_fast_kernel<128,full>",
+                         "kernel": "seg_stats_lean_kernel<128>",
                          "kernel_ms": r["kern_ms"],
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,

@@ -68,6 +68,49 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     v = v + dpp_f64<0x140>(v);
     return (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
 }
+// Whole-wave reductions finished with row_bcast:15 / row_bcast:31 (rows 1,3 then rows 2,3
+// take the previous rows' partials) -- two DPP ops instead of four readlanes and the scalar
+// combine; the result is read from lane 63.  wave_sum_f64_b pairs (r3 + r2) + (r1 + r0),
+// which by commutativity is bitwise wave_sum_f64's (r0 + r1) + (r2 + r3).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_rows(unsigned old, unsigned x) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWS, 0xF, false);
+}
+__device__ __forceinline__ unsigned wave_min_b(unsigned v) {
+    v = min(v, dpp<0xB1>(v));
+    v = min(v, dpp<0x4E>(v));
+    v = min(v, dpp<0x141>(v));
+    v = min(v, dpp<0x140>(v));
+    v = min(v, dpp_rows<0x142, 0xA>(v, v));
+    v = min(v, dpp_rows<0x143, 0xC>(v, v));
+    return rl(v, 63);
+}
+__device__ __forceinline__ unsigned wave_max_b(unsigned v) {
+    v = max(v, dpp<0xB1>(v));
+    v = max(v, dpp<0x4E>(v));
+    v = max(v, dpp<0x141>(v));
+    v = max(v, dpp<0x140>(v));
+    v = max(v, dpp_rows<0x142, 0xA>(v, v));
+    v = max(v, dpp_rows<0x143, 0xC>(v, v));
+    return rl(v, 63);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_rows_f64(double x) {  // 0.0 in the rows not selected
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const unsigned lo = dpp_rows<CTRL, ROWS>(0u, (unsigned)b);
+    const unsigned hi = dpp_rows<CTRL, ROWS>(0u, (unsigned)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_sum_f64_b(double v) {
+    v = v + dpp_f64<0xB1>(v);
+    v = v + dpp_f64<0x4E>(v);
+    v = v + dpp_f64<0x141>(v);
+    v = v + dpp_f64<0x140>(v);
+    v = v + dpp_rows_f64<0x142, 0xA>(v);
+    v = v + dpp_rows_f64<0x143, 0xC>(v);
+    return rl(v, 63);
+}
+
 // Inclusive prefix sum over the 64 lanes: row_shr 1/2/4/8 (bound_ctrl zero-fills
 // lanes whose source is outside the row), then add the preceding rows' totals.
 __device__ __forceinline__ unsigned wave_incl_scan_u32(unsigned v) {
@@ -144,3 +187,4 @@ __device__ __forceinline__ float ns_to_us(unsigned ns) { return (float)ns / 1000
 }  // namespace nvrx
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));

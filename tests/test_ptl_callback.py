@@ -7,13 +7,19 @@ CPU: constructor errors, score formatting, report handling and PTL logging, the 
 broadcast from rank 0 (gloo, ws=2) with the Detector calls replaced by fakes.
 GPU: the reference's two fitting tests (scores printed / logged) on the HIP Detector.
 """
+import json
 import logging
 import math
+import os
+import subprocess
+import sys
 import time
 
 import pytest
 
 from _mp import run_world
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _cb(**kw):
@@ -200,29 +206,70 @@ def _fit(cb, seconds):
     return module, i
 
 
-@pytest.mark.gpu
-def test_prints_perf_scores_when_fitting(log_capture):
+def _fit_in_child(kind):
+    """Run one fitting scenario in a fresh interpreter: kernel-dispatch capture is configured
+    before the process's first HIP call (cupti.enable_capture), as a training script does
+    by initialising the Detector before touching the GPU -- this pytest process has long
+    initialised the runtime, so a Detector created here would capture nothing."""
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(
+        [os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"), os.path.join(ROOT, "tests"),
+         os.environ.get("PYTHONPATH", "")]))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), kind], capture_output=True,
+                       text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _child_main(kind):
+    from nvidia_resiliency_ext.straggler import cupti
+
+    assert cupti.enable_capture(), "capture must configure in a fresh process"
     from nvidia_resiliency_ext import straggler
 
-    module, iters = _fit(_cb(num_gpu_perf_scores_to_print=1, enable_ptl_logging=False), 3.0)
-    assert iters > 16
-    txt = log_capture.text()
-    assert "GPU relative" in txt and "GPU individual" in txt
-    assert "Straggler report processing time" in txt
-    assert module.logged == []
-    assert not straggler.Detector.initialized
+    lg = logging.getLogger("test_logger")
+    h = _ListHandler()
+    lg.addHandler(h)
+    lg.setLevel(logging.DEBUG)
+    if kind == "print":
+        module, iters = _fit(_cb(num_gpu_perf_scores_to_print=1, enable_ptl_logging=False), 3.0)
+    else:
+        module, iters = _fit(_cb(num_gpu_perf_scores_to_print=0, enable_ptl_logging=True), 3.0)
+    print(json.dumps({"iters": iters, "log": h.text(), "logged": module.logged,
+                      "initialized": bool(straggler.Detector.initialized),
+                      "capture": bool(cupti.capture_available())}))
 
 
 @pytest.mark.gpu
-def test_logs_perf_scores_when_fitting(log_capture):
-    module, _ = _fit(_cb(num_gpu_perf_scores_to_print=0, enable_ptl_logging=True), 3.0)
-    txt = log_capture.text()
+def test_prints_perf_scores_when_fitting():
+    res = _fit_in_child("print")
+    assert res["capture"] and res["iters"] > 16
+    txt = res["log"]
+    assert "GPU relative" in txt and "GPU individual" in txt
+    assert "Straggler report processing time" in txt
+    assert "Score=1.00" in txt  # one rank: relative score against itself
+    assert res["logged"] == []
+    assert not res["initialized"]
+
+
+@pytest.mark.gpu
+def test_logs_perf_scores_when_fitting():
+    res = _fit_in_child("log")
+    assert res["capture"]
+    txt = res["log"]
     assert "GPU relative" not in txt and "GPU individual" not in txt
-    assert module.logged, "no scores reached the PTL loggers"
-    keys = set().union(*module.logged)
+    logged = res["logged"]
+    assert logged, "no scores reached the PTL loggers"
+    keys = set().union(*logged)
     assert {"gpu_relative_perf/median", "gpu_individual_perf/max"} <= keys
-    # one rank: every score is 1.0 (relative against itself; individual on first sight)
-    assert all(v == 1.0 for d in module.logged for v in d.values())
+    # one rank: relative scores are 1.0 (against itself); individual scores are 1.0 on
+    # first sight and hist/MED <= 1 afterwards (reporting.py:298-314: history = running min)
+    for d in logged:
+        for k, v in d.items():
+            if k.startswith("gpu_relative_perf/"):
+                assert v == 1.0, (k, v, logged)
+            else:
+                assert 0.0 < v <= 1.0, (k, v, logged)
+    assert logged[1]["gpu_individual_perf/max"] == 1.0  # the first report
 
 
 @pytest.mark.gpu
@@ -247,3 +294,7 @@ def test_training_step_is_wrapped_in_a_detection_section():
     finally:
         cb.teardown(trainer, _Module(), "fit")
     assert strategy.training_step == original
+
+
+if __name__ == "__main__":
+    _child_main(sys.argv[1])

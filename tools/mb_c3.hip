@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "segment_kernels.h"
@@ -31,13 +32,14 @@ __device__ __forceinline__ uint64_t smix(uint64_t x) {
 }
 
 __global__ void gen(uint32_t* ns, int64_t nseg, int S, int K) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nseg * S) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nseg * S;
+       i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t seg = i / S;
     const uint64_t k = (uint64_t)(seg % K);
     const uint64_t base = 2000 + smix(0xBA5E ^ k) % 1998000;
     const uint64_t u = smix(0x5EED ^ (uint64_t)i);
     ns[i] = (uint32_t)(base + (((u >> 32) * (base / 10)) >> 32));
+  }
 }
 
 // G segments per wave, WPB waves per block; loads of all G segments issued first.
@@ -158,19 +160,19 @@ float timeit(F f, int reps) {
     return ms / reps;
 }
 
-int main(int argc, char** argv) {
-    const int64_t R = argc > 1 ? atoll(argv[1]) : 4096, K = 2048;
-    const int S = 1024;
+template <int PL>
+int run(int64_t R, int64_t K, bool prod_data) {
+    const int S = 64 * PL;
     const int64_t nseg = R * K;
     const int reps = 5;
     uint32_t* ns;
     CK(hipMalloc(&ns, (size_t)nseg * S * 4));
-    if (argc > 2 && argv[2][0] == 's') {  // the production generator (libnvrx_synth.so)
+    if (prod_data) {  // the production generator (libnvrx_synth.so)
         if (nvrx_synth_matrix(ns, R, K, K, nullptr, S, 0x5EED, 0xBA5E, nullptr, nullptr) != 0) return 1;
-        std::printf("data: nvrx_synth_matrix\n");
+        std::printf("data: nvrx_synth_matrix R=%ld K=%ld S=%d\n", (long)R, (long)K, S);
     } else {
-        gen<<<(unsigned)((nseg * S + 255) / 256), 256>>>(ns, nseg, S, (int)K);
-        std::printf("data: local gen\n");
+        gen<<<65536, 256>>>(ns, nseg, S, (int)K);
+        std::printf("data: local gen R=%ld K=%ld S=%d\n", (long)R, (long)K, S);
     }
     CK(hipDeviceSynchronize());
     StridedSegs segs{ns, S, 0, S, 8192};
@@ -180,55 +182,51 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&scratch, (size_t)nseg * 4));
     const double gb = (double)nseg * S * 4 / 1e9;
     std::vector<char> h0((size_t)nseg * 24), h1((size_t)nseg * 24);
-
     auto report = [&](const char* name, float ms, bool check) {
-        bool ok = true;
+        const char* verdict = "";
         if (check) {
             CK(hipMemcpy(h0.data(), ref.mem, h0.size(), hipMemcpyDeviceToHost));
             CK(hipMemcpy(h1.data(), got.mem, h1.size(), hipMemcpyDeviceToHost));
-            ok = h0 == h1;
+            verdict = h0 == h1 ? "bit-exact" : "MISMATCH";
+            if (h0 != h1) {
+                for (size_t i = 0; i < h0.size(); i += 4)
+                    if (std::memcmp(&h0[i], &h1[i], 4)) {
+                        std::printf("  first diff at field %zu seg %zu\n", i / 4 / nseg, (i / 4) % nseg);
+                        break;
+                    }
+            }
             CK(hipMemset(got.mem, 0xFF, h1.size()));
         }
-        std::printf("%-28s %8.3f ms %6.2f TB/s %s\n", name, ms, gb / ms, check ? (ok ? "bit-exact" : "MISMATCH") : "");
+        std::printf("%-28s %8.3f ms %6.2f TB/s %s\n", name, ms, gb / ms, verdict);
         std::fflush(stdout);
     };
     const unsigned g4 = (unsigned)((nseg + 3) / 4);
-    report("v0 prod 256thr", timeit([&] {
-               hipLaunchKernelGGL((seg_stats_fast_kernel<16, true, StridedSegs>), dim3(g4), dim3(256), 0, 0, segs, nseg, ref.soa, cr);
-           }, reps), false);
-    report("v1 1 seg/wave 1024thr", timeit([&] {
-               hipLaunchKernelGGL((seg_multi<16, 1, 16>), dim3((unsigned)((nseg + 15) / 16)), dim3(1024), 0, 0, segs, nseg, got.soa, cr);
-           }, reps), true);
-    report("v1b 1 seg/wave 512thr", timeit([&] {
-               hipLaunchKernelGGL((seg_multi<16, 1, 8>), dim3((unsigned)((nseg + 7) / 8)), dim3(512), 0, 0, segs, nseg, got.soa, cr);
-           }, reps), true);
-    report("v2 2 seg/wave 256thr", timeit([&] {
-               hipLaunchKernelGGL((seg_multi<16, 2, 4>), dim3((unsigned)((nseg + 7) / 8)), dim3(256), 0, 0, segs, nseg, got.soa, cr);
-           }, reps), true);
-    report("v2b 2 seg/wave 1024thr", timeit([&] {
-               hipLaunchKernelGGL((seg_multi<16, 2, 16>), dim3((unsigned)((nseg + 31) / 32)), dim3(1024), 0, 0, segs, nseg, got.soa, cr);
-           }, reps), true);
-    report("v2c 4 seg/wave 256thr", timeit([&] {
-               hipLaunchKernelGGL((seg_multi<16, 4, 4>), dim3((unsigned)((nseg + 15) / 16)), dim3(256), 0, 0, segs, nseg, got.soa, cr);
-           }, reps), true);
-    for (int wpc : {8, 16, 32}) {
-        char nm[64];
-        std::snprintf(nm, sizeof nm, "v3 persist %d wg/CU", wpc);
-        report(nm, timeit([&] {
-                   hipLaunchKernelGGL((seg_persist<16, 4>), dim3(256 * wpc), dim3(256), 0, 0, segs, nseg, got.soa, cr);
+    for (int rep = 0; rep < 2; ++rep) {
+        report("v0 fast_body", timeit([&] {
+                   hipLaunchKernelGGL((seg_stats_fast_kernel<PL, true, StridedSegs>), dim3(g4), dim3(256), 0, 0, segs, nseg, ref.soa, cr);
+               }, reps), false);
+        report("v4 lean_body", timeit([&] {
+                   hipLaunchKernelGGL((seg_stats_lean_kernel<PL, StridedSegs>), dim3(g4), dim3(256), 0, 0, segs, nseg, got.soa, cr);
                }, reps), true);
     }
-    report("read-only 256thr", timeit([&] {
-               hipLaunchKernelGGL((read_only<16, 4>), dim3(g4), dim3(256), 0, 0, segs, nseg, scratch);
+    report("read-only", timeit([&] {
+               hipLaunchKernelGGL((read_only<PL, 4>), dim3(g4), dim3(256), 0, 0, segs, nseg, scratch);
            }, reps), false);
-    report("read-only 1024thr", timeit([&] {
-               hipLaunchKernelGGL((read_only<16, 16>), dim3((unsigned)((nseg + 15) / 16)), dim3(1024), 0, 0, segs, nseg, scratch);
-           }, reps), false);
-    report("empty 256thr (dispatch)", timeit([&] {
-               hipLaunchKernelGGL((empty_k<4>), dim3(g4), dim3(256), 0, 0, nseg, scratch);
-           }, reps), false);
-    report("empty 1024thr (dispatch)", timeit([&] {
-               hipLaunchKernelGGL((empty_k<16>), dim3((unsigned)((nseg + 15) / 16)), dim3(1024), 0, 0, nseg, scratch);
-           }, reps), false);
+    CK(hipFree(ns));
+    CK(hipFree(ref.mem));
+    CK(hipFree(got.mem));
+    CK(hipFree(scratch));
     return 0;
+}
+
+int main(int argc, char** argv) {
+    // mb_c3 [R] [s|l] [PL]: R ranks x 2048 kernels x 64*PL samples
+    const int64_t R = argc > 1 ? atoll(argv[1]) : 4096, K = 2048;
+    const bool prod = !(argc > 2 && argv[2][0] == 'l');
+    const int pl = argc > 3 ? atoi(argv[3]) : 16;
+    if (pl == 16) return run<16>(R, K, prod);
+    if (pl == 32) return run<32>(R, K, prod);
+    if (pl == 64) return run<64>(R, K, prod);
+    if (pl == 128) return run<128>(R, K, prod);
+    return 2;
 }

@@ -5,7 +5,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "seg_stats_fast_kernel<128, true, nvrx::StridedSegs>"
+KERNEL = "seg_stats_lean_kernel<128, nvrx::StridedSegs>"
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round"
 
 
