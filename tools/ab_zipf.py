@@ -1,5 +1,6 @@
-"""configs[3] pieces timed in one process: records_bucket, then length-classed stats.
-AB_R ranks (default 16384) of Zipf record streams; prints ms per phase."""
+"""configs[3] record-stream statistics timed alone: MatrixReporter.compute_stats_records
+(bucketing + length-classed statistics) on AB_R ranks (default 16384) of Zipf record
+streams; prints ms per call and the NVRX_* environment it ran under (A/B knobs)."""
 import os
 import sys
 
@@ -8,7 +9,7 @@ sys.path.insert(0, os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from nvidia_resiliency_ext.straggler import batch, ops, synth  # noqa: E402
+from nvidia_resiliency_ext.straggler import batch, synth  # noqa: E402
 
 R, K, CAP = int(os.environ.get("AB_R", 16384)), 2048, 8192
 counts = synth.zipf_counts(K)
@@ -20,18 +21,18 @@ rec_off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * N
 rep = batch.MatrixReporter(R, K, cap=CAP)
 rep.compute_stats_records(recs, rec_off)
 torch.cuda.synchronize()
+ref = rep.stats.cpu()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-b = rep._bucket
-e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-tb = ts = 0.0
+e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+ts = 0.0
 for _ in range(n):
     e[0].record()
-    ops.records_bucket(recs, rec_off, K, CAP, out=b)
+    rep.compute_stats_records(recs, rec_off)
     e[1].record()
-    rep.compute_stats_records(recs, rec_off)  # fused path (bucket + in-block short runs + rest)
-    e[2].record()
     torch.cuda.synchronize()
-    tb += e[0].elapsed_time(e[1])
-    ts += e[1].elapsed_time(e[2])
-print(f"R={R} records={R*N} bucket_ms={tb/n:.3f} ({R*N*16/(tb/n)/1e6:.0f} GB/s at 16 B/rec) "
-      f"fused_records_stats_ms={ts/n:.3f}")
+    ts += e[0].elapsed_time(e[1])
+if os.environ.get("AB_DUMP"):
+    torch.save({f: getattr(ref, f) for f in ("num", "min", "max", "med", "avg", "std")}, os.environ["AB_DUMP"])
+env = {k: v for k, v in os.environ.items() if k.startswith("NVRX_")}
+print(f"R={R} records={R*N} records_stats_ms={ts/n:.3f} "
+      f"({R*N*8/(ts/n)/1e6:.0f} GB/s at 8 B/rec) env={env}")
