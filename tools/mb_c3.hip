@@ -161,10 +161,9 @@ float timeit(F f, int reps) {
 }
 
 template <int PL>
-int run(int64_t R, int64_t K, bool prod_data) {
+int run(int64_t R, int64_t K, bool prod_data, int reps) {
     const int S = 64 * PL;
     const int64_t nseg = R * K;
-    const int reps = 5;
     uint32_t* ns;
     CK(hipMalloc(&ns, (size_t)nseg * S * 4));
     if (prod_data) {  // the production generator (libnvrx_synth.so)
@@ -201,7 +200,7 @@ int run(int64_t R, int64_t K, bool prod_data) {
         std::fflush(stdout);
     };
     const unsigned g4 = (unsigned)((nseg + 3) / 4);
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < 4; ++rep) {
         report("v0 fast_body", timeit([&] {
                    hipLaunchKernelGGL((seg_stats_fast_kernel<PL, true, StridedSegs>), dim3(g4), dim3(256), 0, 0, segs, nseg, ref.soa, cr);
                }, reps), false);
@@ -220,13 +219,14 @@ int run(int64_t R, int64_t K, bool prod_data) {
 }
 
 int main(int argc, char** argv) {
-    // mb_c3 [R] [s|l] [PL]: R ranks x 2048 kernels x 64*PL samples
+    // mb_c3 [R] [s|l] [PL] [reps]: R ranks x 2048 kernels x 64*PL samples
     const int64_t R = argc > 1 ? atoll(argv[1]) : 4096, K = 2048;
     const bool prod = !(argc > 2 && argv[2][0] == 'l');
     const int pl = argc > 3 ? atoi(argv[3]) : 16;
-    if (pl == 16) return run<16>(R, K, prod);
-    if (pl == 32) return run<32>(R, K, prod);
-    if (pl == 64) return run<64>(R, K, prod);
-    if (pl == 128) return run<128>(R, K, prod);
+    const int reps = argc > 4 ? atoi(argv[4]) : 5;
+    if (pl == 16) return run<16>(R, K, prod, reps);
+    if (pl == 32) return run<32>(R, K, prod, reps);
+    if (pl == 64) return run<64>(R, K, prod, reps);
+    if (pl == 128) return run<128>(R, K, prod, reps);
     return 2;
 }
