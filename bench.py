@@ -79,13 +79,20 @@ def make_shard(R, K_global, s_push, world, rank, dev):
     return ns, kidx
 
 
-def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True):
+def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True):
+    """Full reports on one configuration.  use_graph: every report replays the HIP graphs of
+    MatrixReporter.graph (the same kernels; one graph launch instead of one host launch per
+    operation); the stats phase is timed with HIP events between the two replays."""
     R, s_push, cap = cfg["R"], cfg["s_push"], cfg["cap"]
     ns, kidx = make_shard(R, K_global, s_push, world, rank, dev)
     K_local = len(kidx)
     rep = batch.MatrixReporter(R, K_local, cap=cap, thr_rel=THR, thr_ind=THR, device=dev)
     for _ in range(warmup):
         res = rep.report(ns, s_push)
+    g = rep.graph(ns, s_push) if use_graph else None
+    if g is not None:
+        for _ in range(max(1, warmup)):
+            res = g.run()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     barrier(world)
@@ -93,11 +100,17 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True)
     for i in range(steps):
         if time_kernel:
             ev[i][0].record()
-        rep.compute_stats(ns, s_push)
+        if g is not None:
+            g.run_stats()
+        else:
+            rep.compute_stats(ns, s_push)
         if time_kernel:
             ev[i][1].record()
-        rep.compute_scores()
-        res = rep.land()
+        if g is not None:
+            res = g.run_rest()
+        else:
+            rep.compute_scores()
+            res = rep.land()
     barrier(world)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if time_kernel else None
@@ -218,6 +231,7 @@ def main():
     ap.add_argument("--cpu-sample-ranks", type=int, default=16)
     ap.add_argument("--no-zipf", action="store_true")
     ap.add_argument("--zipf-cpu-ranks", type=int, default=1024)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
     args = ap.parse_args()
     rank, world, dev = dist_setup()
     if world != args.gpus:
@@ -225,7 +239,7 @@ def main():
 
     # ---------------- value: configs[1] per GPU, kernel-hash sharded (weak) ----------
     K_global = C2["K"] * world
-    r = run_config(C2, K_global, args.steps, args.warmup, world, rank, dev)
+    r = run_config(C2, K_global, args.steps, args.warmup, world, rank, dev, use_graph=not args.no_graph)
     tmax = allreduce(r["elapsed"], torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
     total_samples = allreduce(float(r["samples"]), torch.distributed.ReduceOp.SUM if world > 1 else None,
                               world, dev)
@@ -243,7 +257,8 @@ def main():
     if not args.no_latency4096:
         del r["ns"]
         torch.cuda.empty_cache()
-        r4 = run_config(C3, C3["K"], max(3, args.steps // 4), 2, world, rank, dev, time_kernel=True)
+        r4 = run_config(C3, C3["K"], max(3, args.steps // 4), 2, world, rank, dev, time_kernel=True,
+                        use_graph=not args.no_graph)
         t4 = allreduce(r4["elapsed"], torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
         tot4 = allreduce(float(r4["samples"]), torch.distributed.ReduceOp.SUM if world > 1 else None,
                          world, dev)
@@ -302,7 +317,7 @@ def main():
                        "ranks": C2["R"], "kernels_per_gpu": C2["K"], "kernels_total": K_global,
                        "samples_pushed": C2["s_push"], "ring_cap": C2["cap"],
                        "parallelism": f"kernel-hash shards x{world}" if world > 1 else "1 GPU",
-                       "stats_mode": "fast"},
+                       "stats_mode": "fast", "launch": "eager" if args.no_graph else "hip_graph"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic,

@@ -714,14 +714,21 @@ __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t
 // ---------------------------------------------------------------------------
 // Host-side launchers shared by segment_stats.hip and segment_ragged.hip
 // ---------------------------------------------------------------------------
-// col_ref: [min med bits | missing] per column, initialised to (+inf, 0) on `st`
+// col_ref: [min med bits | missing] per column, initialised to (+inf, 0) on `st` by one
+// kernel (a launch that HIP graph capture records like any other; template: defined once
+// across the translation units that include this header)
+template <int U = 0>
+__global__ void colref_init_kernel(uint32_t* col_ref, int64_t ncols) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 2 * ncols) col_ref[i] = i < ncols ? 0x7F800000u : 0u;
+}
 static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream_t st, ColRef& cr) {
     cr = ColRef{nullptr, nullptr, 1, 1.0};
     if (!col_ref || ncols <= 0) return hipSuccess;
     cr = ColRef{col_ref, col_ref + ncols, ncols, 1.0 / (double)ncols};
-    hipError_t e = hipMemsetD32Async((hipDeviceptr_t)col_ref, 0x7F800000, (size_t)ncols, st);
-    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(col_ref + ncols), 0, (size_t)ncols, st);
-    return e;
+    hipLaunchKernelGGL(colref_init_kernel<0>, dim3((unsigned)((2 * ncols + 255) / 256)), dim3(256), 0,
+                       st, col_ref, ncols);
+    return hipGetLastError();
 }
 
 template <int PL, class Segs>

@@ -167,6 +167,22 @@ class MatrixReporter:
         """The one device-to-host copy of the packed results, then host views."""
         self.h_out.copy_(self.out, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
+        return self._unpack()
+
+    def report(self, ns: torch.Tensor, s_push: int) -> BatchResult:
+        """One full report: samples resident in HBM -> scores + straggler sets on host."""
+        self.compute_stats(ns, s_push)
+        self.compute_scores()
+        return self.land()
+
+    def graph(self, ns: torch.Tensor, s_push: int) -> "ReportGraph":
+        """The report's device work captured once as HIP graphs, replayed per report (the
+        launch sequence -- reference init, stats, scores, result copy -- costs one graph
+        launch instead of one host launch per operation).  1 GPU, or the stats phase only
+        on N GPUs (the partials exchange stays an eager collective)."""
+        return ReportGraph(self, ns, s_push)
+
+    def _unpack(self) -> BatchResult:
         R = self.R
         h = self.h_out.numpy()
         gr = h[0:8 * R].view(np.float64).copy() if self.relative else None
@@ -175,8 +191,45 @@ class MatrixReporter:
         si = h[17 * R:18 * R].astype(bool) if self.individual else None
         return BatchResult(gr, gi, sr, si, int(h[self._e:self._e + 4].view(np.int32)[0]))
 
-    def report(self, ns: torch.Tensor, s_push: int) -> BatchResult:
-        """One full report: samples resident in HBM -> scores + straggler sets on host."""
-        self.compute_stats(ns, s_push)
-        self.compute_scores()
-        return self.land()
+
+class ReportGraph:
+    """Two HIP graphs over a MatrixReporter's fixed buffers: ``stats`` (column-reference
+    init + the segment statistics kernel) and ``rest`` (scores + straggler masks + the
+    device-to-host copy of the packed results; 1 GPU only).  ``run()`` replays them on the
+    current stream; a caller may record events between the two to time the stats phase."""
+
+    def __init__(self, rep: MatrixReporter, ns: torch.Tensor, s_push: int):
+        self.rep = rep
+        side = torch.cuda.Stream(rep.device)
+        side.wait_stream(torch.cuda.current_stream(rep.device))
+        with torch.cuda.stream(side):  # one eager pass: first-launch setup outside the capture
+            rep.compute_stats(ns, s_push)
+            if rep.world == 1:
+                rep.compute_scores()
+        torch.cuda.current_stream(rep.device).wait_stream(side)
+        torch.cuda.synchronize(rep.device)
+        self.stats = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.stats):
+            rep.compute_stats(ns, s_push)
+        self.rest = None
+        if rep.world == 1:
+            self.rest = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.rest):
+                rep.compute_scores()
+                rep.h_out.copy_(rep.out, non_blocking=True)
+
+    def run_stats(self) -> None:
+        self.stats.replay()
+
+    def run_rest(self) -> BatchResult:
+        rep = self.rep
+        if self.rest is None:
+            rep.compute_scores()
+            return rep.land()
+        self.rest.replay()
+        torch.cuda.current_stream(rep.device).synchronize()
+        return rep._unpack()
+
+    def run(self) -> BatchResult:
+        self.run_stats()
+        return self.run_rest()

@@ -107,3 +107,25 @@ def test_zipf_order_is_a_valid_interleaving():
     slot, occ = synth.zipf_order(counts)
     for k in (0, 1, 7, 100, 2047):
         assert np.array_equal(occ[slot == k], np.arange(counts[k]))  # push order per kernel
+
+
+def test_graph_replay_matches_eager():
+    # MatrixReporter.graph: the same kernels captured once and replayed; three successive
+    # reports (history carried) equal the eager reporter's bit for bit
+    R, K, S, cap = 48, 300, 700, 512
+    ns = synth.synth_matrix(R, K, S)
+    eager = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    graphed = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    g = graphed.graph(ns, S)
+    graphed.reset_history()  # the capture's eager warm pass updated the history once
+    for _ in range(3):
+        a = eager.report(ns, S)
+        b = g.run()
+        assert np.array_equal(a.gpu_relative, b.gpu_relative)
+        assert np.array_equal(a.gpu_individual, b.gpu_individual)
+        assert np.array_equal(a.stragglers_relative, b.stragglers_relative)
+        assert np.array_equal(a.stragglers_individual, b.stragglers_individual)
+        assert a.err == b.err == 0
+    for f in ("num", "min", "max", "med", "avg", "std"):
+        assert torch.equal(getattr(eager.stats, f), getattr(graphed.stats, f)), f
+    assert torch.equal(eager.hist, graphed.hist)
