@@ -1,4 +1,4 @@
-// mb_c3.hip -- microbenchmark of launch shapes for the C3 stats kernel (4096 x 2048 x 1024
+// mb_c3.hip -- microbenchmark of launch shapes for the strided stats kernel (default C3: 4096 x 2048 x 1024
 // u32 samples, one 4 KB segment per wave).  Builds against csrc/segment_kernels.h; every
 // variant's outputs are compared bit for bit with the production kernel's.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I../nvidia-resiliency-ext-x_amd/csrc
@@ -71,6 +71,35 @@ void seg_multi(StridedSegs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
     }
 }
 
+// G segments per wave through lean_body, all G segments' loads issued first
+template <int PL, int G, int WPB, int OCC>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC)))
+void lean_multi(StridedSegs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
+    constexpr int NB = Bins<PL>::NB;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[WPB * NB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    unsigned* hist = lds_hist + wave * NB;
+    const int64_t s0 = ((int64_t)blockIdx.x * WPB + wave) * G;
+    unsigned v[G][PL];
+    const uint32_t* p[G];
+    int n[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if (s0 + g < nseg) {
+            segs.get(s0 + g, p[g], n[g]);
+            issue_loads<PL>(p[g], n[g], v[g]);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if (s0 + g >= nseg) return;
+        int m0;
+        unsigned x0;
+        finish_loads<PL, true>(p[g], n[g], v[g], m0, x0);
+        lean_body<PL>(v[g], n[g], x0, s0 + g, hist, out, cr);
+    }
+}
+
 // persistent: each wave walks segments w, w + W, ... with the next segment's loads in flight
 template <int PL, int WPB>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(6)))
@@ -99,6 +128,43 @@ void seg_persist(StridedSegs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) 
         unsigned x0;
         finish_loads<PL, true>(p, n, a, m0, x0);
         fast_body<PL, true>(a, n, m0, x0, s, hist, out, cr);
+        if (sn >= nseg) return;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) a[i] = b[i];
+        s = sn;
+        p = pn;
+        n = nn;
+    }
+}
+
+// persistent lean waves, next segment's loads in flight while the current one is reduced
+template <int PL, int WPB, int OCC>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(OCC)))
+void lean_persist(StridedSegs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
+    constexpr int NB = Bins<PL>::NB;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[WPB * NB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    unsigned* hist = lds_hist + wave * NB;
+    const int64_t W = (int64_t)gridDim.x * WPB;
+    int64_t s = (int64_t)blockIdx.x * WPB + wave;
+    if (s >= nseg) return;
+    unsigned a[PL], b[PL];
+    const uint32_t* p;
+    int n;
+    segs.get(s, p, n);
+    issue_loads<PL>(p, n, a);
+    for (;;) {
+        const int64_t sn = s + W;
+        const uint32_t* pn = p;
+        int nn = n;
+        if (sn < nseg) {
+            segs.get(sn, pn, nn);
+            issue_loads<PL>(pn, nn, b);
+        }
+        int m0;
+        unsigned x0;
+        finish_loads<PL, true>(p, n, a, m0, x0);
+        lean_body<PL>(a, n, x0, s, hist, out, cr);
         if (sn >= nseg) return;
 #pragma unroll
         for (int i = 0; i < PL; ++i) a[i] = b[i];
@@ -207,6 +273,17 @@ int run(int64_t R, int64_t K, bool prod_data, int reps) {
         report("v4 lean_body", timeit([&] {
                    hipLaunchKernelGGL((seg_stats_lean_kernel<PL, StridedSegs>), dim3(g4), dim3(256), 0, 0, segs, nseg, got.soa, cr);
                }, reps), true);
+        if (PL <= 32) {
+            report("m2o8 lean 2 seg/wave occ8", timeit([&] {
+                       hipLaunchKernelGGL((lean_multi<PL, 2, 4, 8>), dim3((unsigned)((nseg + 7) / 8)), dim3(256), 0, 0, segs, nseg, got.soa, cr);
+                   }, reps), true);
+            report("m2o6 lean 2 seg/wave occ6", timeit([&] {
+                       hipLaunchKernelGGL((lean_multi<PL, 2, 4, 6>), dim3((unsigned)((nseg + 7) / 8)), dim3(256), 0, 0, segs, nseg, got.soa, cr);
+                   }, reps), true);
+            report("m4o4 lean 4 seg/wave occ4", timeit([&] {
+                       hipLaunchKernelGGL((lean_multi<PL, 4, 4, 4>), dim3((unsigned)((nseg + 15) / 16)), dim3(256), 0, 0, segs, nseg, got.soa, cr);
+                   }, reps), true);
+        }
     }
     report("read-only", timeit([&] {
                hipLaunchKernelGGL((read_only<PL, 4>), dim3(g4), dim3(256), 0, 0, segs, nseg, scratch);
