@@ -179,10 +179,16 @@ __device__ __forceinline__ void lane_sums_f64(const unsigned (&v)[PL], uint64_t&
     sq = q0 + q1;
 }
 
-// CuptiProfiler.cpp:187 -- (end - start) / 1000.0f: integer ns -> f32 (round to
-// nearest) -> correctly-rounded IEEE divide (hipcc lowers '/' to the
-// div_scale/div_fmas/div_fixup sequence; the build never enables fast-math).
-__device__ __forceinline__ float ns_to_us(unsigned ns) { return (float)ns / 1000.0f; }
+// CuptiProfiler.cpp:187 -- (end - start) / 1000.0f: integer ns -> f32 (round to nearest),
+// then the correctly rounded f32 quotient by 1000.  Computed as one f64 multiply by
+// RN(1/1000) rounded to f32 (4 VALU instead of the 11-instruction f32 divide sequence):
+// x = f32(ns) is exact in f64 and the product is within 2^-52 relative of x/1000, while
+// x/1000 is never an f32 rounding midpoint (its odd part would need > 24 bits) and lies at
+// least 2^-24 relative away from every other one, so both round to the same f32.  Checked
+// exhaustively for all 2^32 inputs (tests/test_oracle_golden.py re-checks a sample).
+__device__ __forceinline__ float ns_to_us(unsigned ns) {
+    return (float)((double)(float)ns * (1.0 / 1000.0));
+}
 
 }  // namespace nvrx
 

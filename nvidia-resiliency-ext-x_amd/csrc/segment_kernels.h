@@ -356,7 +356,7 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
 
     // ---- exact sum + squares about the pivot c (lane_sums order: pairs, groups of 16) ----
     unsigned c = x0 - mn;
-    double sdl, acc;
+    double sd, acc;
     if (range < (1u << 24)) {
         constexpr int G = PL < 16 ? PL : 16;
         unsigned ls = 0;
@@ -374,7 +374,18 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
             }
             acc += (double)q.x + (double)q.y;
         }
-        sdl = (double)ls;
+        if (PL <= 16) {
+            // integer reduction: a row of 16 lanes sums to < 16 * 16 * 2^24 = 2^32 (no
+            // u32 wrap), the four row sums combine in 64 bits -- exact, as the f64 sum
+            unsigned r = ls;
+            r += dpp<0xB1>(r);
+            r += dpp<0x4E>(r);
+            r += dpp<0x141>(r);
+            r += dpp<0x140>(r);
+            sd = (double)(((uint64_t)rl(r, 0) + rl(r, 16)) + ((uint64_t)rl(r, 32) + rl(r, 48)));
+        } else {
+            sd = wave_sum_f64_b((double)ls);
+        }
     } else {  // rare: a ring spanning >= 16.7 ms -- fast_body's sums
         uint64_t sdi;
         if (range < 0x80000000u) {
@@ -383,9 +394,8 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
             c = 0u;
             lane_sums_f64<PL>(v, sdi, acc);
         }
-        sdl = (double)sdi;
+        sd = wave_sum_f64_b((double)sdi);
     }
-    const double sd = wave_sum_f64_b(sdl);
     const double sq = wave_sum_f64_b(acc);
 
     // ---- first histogram level ----
@@ -449,9 +459,19 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
             __builtin_amdgcn_wave_barrier();
             const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
             unsigned rank = 0;
-            for (int j = 0; j < (int)n0; ++j) {
-                const unsigned cj = __builtin_amdgcn_readlane(ci, j);
-                rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
+            if (shift <= 26) {
+                // unique keys (candidate - lo0, lane) in one word: rank = keys below mine, one
+                // compare per candidate; lanes >= n0 hold the maximum and never count
+                const unsigned key = (lane < (int)n0) ? ((ci - lo0) << 6) | (unsigned)lane : 0xFFFFFFFFu;
+                for (int j = 0; j < (int)n0; j += 4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) rank += (rl(key, j + u) < key) ? 1u : 0u;
+                }
+            } else {
+                for (int j = 0; j < (int)n0; ++j) {
+                    const unsigned cj = __builtin_amdgcn_readlane(ci, j);
+                    rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
+                }
             }
             const unsigned r0 = t0 - below - c0, r1 = t1 - below - c0;
             const int L0 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r0)) - 1;

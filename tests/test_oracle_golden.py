@@ -145,3 +145,20 @@ def test_oracle_report_matches_reference(scname):
     if sc["gather"] or "relative_perf_scores" in sc["scores"]:
         assert world.mapper.kernel_name_to_id == fx["name_mapper"]["kernel"]
         assert world.mapper.section_name_to_id == fx["name_mapper"]["section"]
+
+
+def test_ns_to_us_reciprocal_multiply_identity():
+    # the kernels convert ns -> us as f32(f64(f32(ns)) * RN(1/1000)) (nvrx_common.h ns_to_us);
+    # that equals the reference's correctly rounded f32(ns) / 1000.0f (CuptiProfiler.cpp:187)
+    # for every u32 -- checked exhaustively offline; here 2^24 random values plus the edges
+    rng = np.random.default_rng(187)
+    x = np.concatenate([
+        rng.integers(0, 2**32, size=1 << 24, dtype=np.uint64).astype(np.uint32),
+        np.arange(0, 1 << 16, dtype=np.uint32),
+        (np.uint64(1) << np.arange(32, dtype=np.uint64)).astype(np.uint32),
+        np.array([2**24 - 1, 2**24 + 1, 2**24 + 3, 2**32 - 1, 2**31 - 1, 999, 1000, 1001],
+                 dtype=np.uint32)])
+    f = x.astype(np.float32)
+    ref = f / np.float32(1000.0)
+    got = (f.astype(np.float64) * (1.0 / 1000.0)).astype(np.float32)
+    assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
