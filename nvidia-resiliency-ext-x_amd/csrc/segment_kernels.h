@@ -167,6 +167,39 @@ __device__ __forceinline__ void hist_locate2(const unsigned* hist, unsigned ta, 
     cb = __builtin_amdgcn_readlane(nb, Lb);
 }
 
+// One target: bucket holding relative rank ta, elements below it, and its count.
+template <int PL>
+__device__ __forceinline__ void hist_locate1(const unsigned* hist, unsigned ta, unsigned& ba,
+                                             unsigned& bfa, unsigned& ca) {
+    constexpr int BPL = Bins<PL>::BPL;
+    const int lane = lane_id();
+    unsigned h[BPL];
+    unsigned local = 0;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        h[j] = hist[lane * BPL + j];
+        local += h[j];
+    }
+    const unsigned incl = wave_incl_scan_u32(local);
+    const int La = __popcll(__ballot(incl <= ta));
+    unsigned run = incl - local, sa = 0, pa = 0, na = 0;
+    bool fa = false;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        const unsigned nxt = run + h[j];
+        if (!fa && nxt > ta) {
+            fa = true;
+            sa = (unsigned)(lane * BPL + j);
+            pa = run;
+            na = h[j];
+        }
+        run = nxt;
+    }
+    ba = __builtin_amdgcn_readlane(sa, La);
+    bfa = __builtin_amdgcn_readlane(pa, La);
+    ca = __builtin_amdgcn_readlane(na, La);
+}
+
 // Occupancy target per PL: the samples take PL VGPRs; ask the register allocator for
 // enough waves per SIMD that HBM latency is covered by other waves' segments.
 template <int PL>
@@ -424,8 +457,16 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
             }
             __builtin_amdgcn_wave_barrier();
         }
-        unsigned b0, c0, n0, b1, c1, n1;
-        hist_locate2<PL>(hist, t0 - below, t1 - below, b0, c0, n0, b1, c1, n1);
+        // rank t1 = t0 or t0 + 1: usually in t0's bucket, so locate t0 alone and t1 only
+        // when it lies past that bucket (a wave-uniform branch)
+        unsigned b0, c0, n0, b1;
+        hist_locate1<PL>(hist, t0 - below, b0, c0, n0);
+        if (t1 - below < c0 + n0) {
+            b1 = b0;
+        } else {
+            unsigned c1, n1;
+            hist_locate1<PL>(hist, t1 - below, b1, c1, n1);
+        }
         if (b0 != b1) {
             const unsigned hi0 = wlo + ((b0 + 1) << shift);
             const unsigned lo1 = wlo + (b1 << shift);
