@@ -295,8 +295,14 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
             }
             __builtin_amdgcn_wave_barrier();
         }
-        unsigned b0, c0, n0, b1, c1, n1;
-        hist_locate2<PL>(hist, t0 - below, t1 - below, b0, c0, n0, b1, c1, n1);
+        unsigned b0, c0, n0, b1;  // t1 is t0 or t0 + 1: located only past t0's bucket
+        hist_locate1<PL>(hist, t0 - below, b0, c0, n0);
+        if (t1 - below < c0 + n0) {
+            b1 = b0;
+        } else {
+            unsigned c1, n1;
+            hist_locate1<PL>(hist, t1 - below, b1, c1, n1);
+        }
         if (b0 != b1) {
             // s[t0] is the largest sample of bucket b0, s[t1] the smallest of bucket b1
             unsigned lmax = 0, lmin = 0xFFFFFFFFu;
@@ -333,9 +339,17 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
             __builtin_amdgcn_wave_barrier();
             const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
             unsigned rank = 0;
-            for (int j = 0; j < (int)n0; ++j) {
-                const unsigned cj = __builtin_amdgcn_readlane(ci, j);
-                rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
+            if (shift <= 26) {  // one-compare unique keys, as in lean_body
+                const unsigned key = (lane < (int)n0) ? ((ci - lo0) << 6) | (unsigned)lane : 0xFFFFFFFFu;
+                for (int j = 0; j < (int)n0; j += 4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) rank += (rl(key, j + u) < key) ? 1u : 0u;
+                }
+            } else {
+                for (int j = 0; j < (int)n0; ++j) {
+                    const unsigned cj = __builtin_amdgcn_readlane(ci, j);
+                    rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
+                }
             }
             const unsigned r0 = t0 - below - c0, r1 = t1 - below - c0;
             const int L0 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r0)) - 1;
