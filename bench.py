@@ -293,6 +293,34 @@ def main():
                         0 if args.no_cpu_baseline else args.zipf_cpu_ranks, threads)
         torch.cuda.empty_cache()
 
+    # ---------------- configs[0] shape: a small world's report latency (rank 0, N == 1) ----
+    # 8 ranks x 200 kernels x 1000 samples (the reference's CPU/gloo case, BASELINE.md: 29.1 ms
+    # per report in the survey container): the whole HIP report vs the CPU restatement
+    # (computeStats + scoring) on the same inputs
+    c1 = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        C1 = dict(R=8, K=200, s_push=1000, cap=8192)
+        n1 = 50
+        r1 = run_config(C1, C1["K"], n1, 5, 1, 0, dev, time_kernel=False, use_graph=not args.no_graph)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        host = r1["ns"].contiguous().cpu().numpy().view(np.uint32).reshape(-1)
+        t1 = time.perf_counter()
+        reps1 = 20
+        for _ in range(reps1):
+            st1 = O.matrix_stats(host, C1["R"] * C1["K"], C1["s_push"], 0, C1["s_push"], C1["cap"],
+                                 nthreads=min(8, threads))
+            gr1, _ = O.scores(st1["num"].reshape(C1["R"], C1["K"]), st1["med"].reshape(C1["R"], C1["K"]),
+                              st1["avg"].reshape(C1["R"], C1["K"]))
+            O.stragglers(gr1, THR)
+        cpu_ms = (time.perf_counter() - t1) / reps1 * 1e3
+        c1 = dict(ranks=C1["R"], kernels=C1["K"], samples_per_kernel=C1["s_push"],
+                  gpu_ms_per_report=r1["elapsed"] / n1 * 1e3,
+                  cpu_port_ms_per_report=cpu_ms, cpu_port_cores=min(8, threads),
+                  reference_survey_ms_per_report=29.1,
+                  gpu_relative_matches_cpu=bool(np.allclose(r1["res"].gpu_relative, gr1, rtol=1e-6)))
+        del r1
+
     # ---------------- CPU baseline (rank 0, N == 1 only) ------------------------------
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -338,6 +366,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,
+            "configs0_report": c1,
             "zipf_16384_ranks": zipf,
             "straggler_sets_exact": sets_ok,
         }
