@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -254,11 +255,24 @@ int run(int64_t R, int64_t K, bool prod_data, int reps) {
             CK(hipMemcpy(h1.data(), got.mem, h1.size(), hipMemcpyDeviceToHost));
             verdict = h0 == h1 ? "bit-exact" : "MISMATCH";
             if (h0 != h1) {
-                for (size_t i = 0; i < h0.size(); i += 4)
-                    if (std::memcmp(&h0[i], &h1[i], 4)) {
-                        std::printf("  first diff at field %zu seg %zu\n", i / 4 / nseg, (i / 4) % nseg);
-                        break;
+                // per field: differing segments; for the float fields the largest relative diff
+                for (int f = 0; f < 6; ++f) {
+                    size_t nd = 0;
+                    double rel = 0.0;
+                    for (int64_t k = 0; k < nseg; ++k) {
+                        const size_t i = ((size_t)f * nseg + k) * 4;
+                        if (std::memcmp(&h0[i], &h1[i], 4) == 0) continue;
+                        ++nd;
+                        if (f > 0) {
+                            float a, b;
+                            std::memcpy(&a, &h0[i], 4);
+                            std::memcpy(&b, &h1[i], 4);
+                            const double r = std::fabs((double)a - (double)b) / std::fabs((double)a);
+                            if (r > rel) rel = r;
+                        }
                     }
+                    if (nd) std::printf("  field %d: %zu segments differ, max rel %.3g\n", f, nd, rel);
+                }
             }
             CK(hipMemset(got.mem, 0xFF, h1.size()));
         }
