@@ -81,3 +81,44 @@ def test_config2_full_size():
     _check_mean_std(host.reshape(len(rows) * K, S), g, idx)
     del ns, rep
     torch.cuda.empty_cache()
+
+
+def test_config3_full_size():
+    # configs[3]: 16,384 Zipf record streams.  A few whole streams against the oracle's
+    # ring-push + computeStats restatement; every stream reversed (push order is free when no
+    # ring overflows: kernel 1 is pushed exactly cap = 8192 times) gives the same statistics
+    R, K, cap = 16384, 2048, 8192
+    counts = synth.zipf_counts(K)
+    slot, occ = synth.zipf_order(counts)
+    N = slot.size
+    t = lambda a: torch.from_numpy(a.view(np.int32)).cuda()  # noqa: E731
+    recs = synth.synth_records(R, t(slot), t(occ), K, int(counts.max()))
+    rec_off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * N
+    rep = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    res = rep.report_records(recs, rec_off)
+    assert np.array_equal(res.stragglers_relative, synth.straggler_ranks(R).astype(bool))
+    a = _stats_host(rep)
+    rows = [0, int(np.nonzero(synth.straggler_ranks(R))[0][0]), R - 1]
+    for r in rows:
+        h = recs[r * N:(r + 1) * N].cpu().numpy().view(np.uint32)
+        ref = O.records_stats(h, np.array([0, N], np.int64), K, cap=cap, nthreads=8)
+        sl = slice(r * K, (r + 1) * K)
+        for f in ("num", "min", "max", "med"):
+            assert np.array_equal(a[f][sl].view(np.uint32), ref[f].view(np.uint32)), (r, f)
+        short = ref["num"] <= 64  # lane classes: every field bit-exact
+        for f in ("avg", "std"):
+            assert np.array_equal(a[f][sl][short].view(np.uint32), ref[f][short].view(np.uint32)), (r, f)
+    rev = torch.flip(recs.view(R, N, 2), dims=[1]).reshape(R * N, 2)
+    del recs
+    rep2 = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    res2 = rep2.report_records(rev, rec_off)
+    b = _stats_host(rep2)
+    for f in ("num", "min", "max", "med"):
+        assert np.array_equal(a[f].view(np.uint32), b[f].view(np.uint32)), f
+    short = a["num"] <= 64
+    for f in ("avg", "std"):
+        assert np.array_equal(a[f][short].view(np.uint32), b[f][short].view(np.uint32)), f
+        np.testing.assert_allclose(b[f], a[f], rtol=2.5e-7, atol=0)
+    np.testing.assert_allclose(res2.gpu_relative, res.gpu_relative, rtol=1e-12)
+    del rev, rep, rep2
+    torch.cuda.empty_cache()
