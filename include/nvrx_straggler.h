@@ -122,7 +122,7 @@ int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_str
  * seg_off has nseg+1 entries and segment s ends at seg_off[s+1]); max_len bounds every
  * segment length (host-known); aligned16 != 0 promises every retained run starts on a
  * 16-byte boundary; seg_len[s] < 0 skips segment s (outputs untouched).  col_ref / ncols:
- * as for the strided call (segment s is row s / ncols, column s % ncols).  Segments of <= 64 retained samples are bit-exact in every field in
+ * as for the strided call (segment s is row s / ncols, column s % ncols).  Segments of <= 128 retained samples are bit-exact in every field in
  * both modes (one lane per segment, the reference's sequential f32 sums). */
 int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
                               int64_t nseg, int64_t max_len, int64_t cap, int32_t mode,
@@ -188,7 +188,7 @@ int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t
                         uint32_t* out_ns, int32_t* counts, void* stream);
 /* The whole per-(stream, slot) statistics of record streams (ring retention +
  * CuptiProfiler::getStats for every stream): nvrx_records_bucket, then
- * nvrx_segment_stats_ragged(aligned16) over the buckets (runs of <= 64 samples bit-exact in
+ * nvrx_segment_stats_ragged(aligned16) over the buckets (runs of <= 128 samples bit-exact in
  * every field).  out->* are [nstreams*nslots]; max_len bounds every stream's length
  * (host-known); col_ref (optional, [2*nslots]) as for nvrx_segment_stats_strided (rows =
  * streams), produced by a column reduction. */

@@ -8,7 +8,7 @@
 // classes and each class runs the kernel shaped for it:
 //
 //   n == 0            classifier writes the empty KernelStats (num 0, NaN) itself
-//   n <= 8 / 32 / 64  one LANE per segment: the samples in registers, a bitonic
+//   n <= 8/32/64/128  one LANE per segment: the samples in registers, a bitonic
 //                     sorting network, then CuptiProfiler.cpp:53-71 statement by
 //                     statement (sequential f32 sums) -- every field bit-exact
 //   n <= 64*PL        one WAVE per segment (fast_body, segment_kernels.h), PL 4..128
@@ -28,7 +28,7 @@ namespace nvrx {
 namespace {
 
 enum : int {
-    C_T8 = 0, C_T32, C_T64,                   // lane classes
+    C_T8 = 0, C_T32, C_T64, C_T128,           // lane classes
     C_W4, C_W8, C_W16, C_W32, C_W64, C_W128,  // wave classes (PL)
     C_X,                                      // workgroup (EXACT kernel)
     NCLASS
@@ -41,6 +41,7 @@ __device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
     if (n <= 8) return C_T8;
     if (n <= 32) return C_T32;
     if (n <= 64) return C_T64;
+    if (n <= 128) return C_T128;
     if (exact) return C_X;
     const int need = aligned16 ? n : n + 3;
     if (need <= 64 * 4) return C_W4;
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
 // ---------------------------------------------------------------- lane classes
 template <int N>
 struct LaneOcc {
-    static constexpr int W = N >= 64 ? 4 : N >= 32 ? 6 : 8;
+    static constexpr int W = N >= 128 ? 2 : N >= 64 ? 4 : N >= 32 ? 6 : 8;
 };
 
 // One lane per segment of 1..N samples.  u32 -> f32 us is monotone, so sorting the
@@ -395,15 +396,16 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     launch_lane<8>(segs, list, c + 2 * C_T8, aligned16, out, cr, st);
     if (keep > 8) launch_lane<32>(segs, list, c + 2 * C_T32, aligned16, out, cr, st);
     if (keep > 32) launch_lane<64>(segs, list, c + 2 * C_T64, aligned16, out, cr, st);
+    if (keep > 64) launch_lane<128>(segs, list, c + 2 * C_T128, aligned16, out, cr, st);
     if (!exact) {
-        if (keep > 64) launch_list<4>(segs, list, c + 2 * C_W4, out, cr, st);
+        if (keep > 128) launch_list<4>(segs, list, c + 2 * C_W4, out, cr, st);
         if (need > 64 * 4) launch_list<8>(segs, list, c + 2 * C_W8, out, cr, st);
         if (need > 64 * 8) launch_list<16>(segs, list, c + 2 * C_W16, out, cr, st);
         if (need > 64 * 16) launch_list<32>(segs, list, c + 2 * C_W32, out, cr, st);
         if (need > 64 * 32) launch_list<64>(segs, list, c + 2 * C_W64, out, cr, st);
         if (need > 64 * 64) launch_list<128>(segs, list, c + 2 * C_W128, out, cr, st);
     }
-    if (exact ? keep > 64 : need > 64 * 128) {
+    if (exact ? keep > 128 : need > 64 * 128) {
         if (hipError_t e = launch_exact_list(segs, list, c + 2 * C_X, keep, out, cr, st); e != hipSuccess)
             return e;
     }

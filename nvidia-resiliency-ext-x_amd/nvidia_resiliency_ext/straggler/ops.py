@@ -77,7 +77,7 @@ def segment_stats_ragged(ns: torch.Tensor, seg_off: torch.Tensor, seg_len: Optio
                          max_len: int, cap: int = 0, mode: int = STATS_FAST, aligned16: bool = False,
                          out: Optional[SegmentStats] = None, col_ref: Optional[torch.Tensor] = None,
                          ncols: int = 0, stream=None) -> SegmentStats:
-    """Stats of ragged segments; segments of <= 64 retained samples are bit-exact in every
+    """Stats of ragged segments; segments of <= 128 retained samples are bit-exact in every
     field.  col_ref ([2*ncols] int32): fused per-column reference, as for the strided call."""
     N.require_device(ns, "ns")
     N.require_device(seg_off, "seg_off")

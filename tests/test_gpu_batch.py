@@ -87,7 +87,7 @@ def test_zipf_record_streams_match_oracle(R, cap):
     for f in ("num", "min", "max", "med"):
         a, b = getattr(g, f).numpy(), ref[f]
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), f
-    small = ref["num"] <= 64  # lane classes: every field bit-exact
+    small = ref["num"] <= 128  # lane classes: every field bit-exact
     for f in ("avg", "std"):
         a, b = getattr(g, f).numpy(), ref[f]
         assert np.array_equal(a[small].view(np.uint32), b[small].view(np.uint32)), f
