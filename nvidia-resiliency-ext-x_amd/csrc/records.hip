@@ -86,6 +86,7 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
     uint32_t* start = lds + 2 * nslots; // [nslots] bucket start (relative to stream base) | RB_OVF
     __shared__ uint32_t any_ovf;
+    __shared__ uint32_t wtot[RB_WAVES];
     const int64_t t = blockIdx.x;
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
@@ -110,23 +111,39 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     });
     __syncthreads();
 
-    // exclusive scan of padded keeps over slots (wave 0), 64 at a time with a carry
-    if (wave == 0) {
+    // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
+    // block's other waves would otherwise wait at the barrier while one wave walks all the
+    // slots: with one block per CU that wait was ~1 ms of configs[3]):
+    //   (a) chunk totals -> LDS, (b) each wave scans its chunk from the preceding totals
+    const auto keep_of = [&](uint32_t total) {
+        return (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+    };
+    const int64_t chunk = ((nslots + RB_WAVES - 1) / RB_WAVES + 63) & ~(int64_t)63;
+    const int64_t c_lo = min(nslots, chunk * wave), c_hi = min(nslots, c_lo + chunk);
+    {
+        uint32_t part = 0;
+        for (int64_t s = c_lo + lane; s < c_hi; s += 64) part += (keep_of(cnt[s]) + 3u) & ~3u;
+        part = wave_sum_u32(part);
+        if (lane == 0) wtot[wave] = part;
+    }
+    __syncthreads();
+    {
         uint32_t carry = 0;
+        for (int w = 0; w < wave; ++w) carry += wtot[w];
         bool overflow = false;
-        for (int64_t c = 0; c < nslots; c += 64) {
+        for (int64_t c = c_lo; c < c_hi; c += 64) {
             const int64_t s = c + lane;
             uint32_t keep = 0, total = 0;
-            if (s < nslots) {
+            if (s < c_hi) {
                 total = cnt[s];
-                keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+                keep = keep_of(total);
             }
             const bool ovf = keep != total;
             overflow |= ovf;
             const uint32_t padded = (keep + 3u) & ~3u;
             const uint32_t incl = wave_incl_scan_u32(padded);
             const uint32_t st = carry + incl - padded;
-            if (s < nslots) {
+            if (s < c_hi) {
                 start[s] = st | (ovf || force_stable ? RB_OVF : 0u);
                 const int64_t g = t * nslots + s;
                 seg_off[g] = base + st;
