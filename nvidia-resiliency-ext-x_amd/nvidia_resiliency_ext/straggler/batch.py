@@ -19,6 +19,7 @@ and the history are shard-local and the only exchange is the [R][6] f64 partials
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -34,6 +35,23 @@ from . import ops
 # (kernel_ref: 64 rows per thread, R/64 atomics per column) once R is in the hundreds
 # (measured on MI355X: 885k segments on 54 columns, 0.6 ms -> 4.3 ms fused).
 FUSED_REF_MAX_ROWS = 256
+
+
+def _wait(device) -> None:
+    """Wait for the current stream by polling an event (the report's results land in pinned
+    host memory; a blocking synchronize adds the driver's wake-up latency to every report).
+    NVRX_SYNC=block restores the blocking wait."""
+    st = torch.cuda.current_stream(device)
+    if _SYNC_BLOCK:
+        st.synchronize()
+        return
+    ev = torch.cuda.Event()
+    ev.record(st)
+    while not ev.query():
+        pass
+
+
+_SYNC_BLOCK = os.environ.get("NVRX_SYNC", "") == "block"
 
 
 @dataclass
@@ -166,7 +184,7 @@ class MatrixReporter:
     def land(self) -> BatchResult:
         """The one device-to-host copy of the packed results, then host views."""
         self.h_out.copy_(self.out, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
+        _wait(self.device)
         return self._unpack()
 
     def report(self, ns: torch.Tensor, s_push: int) -> BatchResult:
@@ -227,7 +245,7 @@ class ReportGraph:
             rep.compute_scores()
             return rep.land()
         self.rest.replay()
-        torch.cuda.current_stream(rep.device).synchronize()
+        _wait(rep.device)
         return rep._unpack()
 
     def run(self) -> BatchResult:
