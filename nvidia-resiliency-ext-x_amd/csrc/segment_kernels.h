@@ -91,14 +91,15 @@ __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, i
     const float med = (n & 1) ? f0 : (f0 + f1) / 2;
     const double dn = (double)n;
     const double se = sd - dn * (double)c;  // exact: integers < 2^53
-    double num;
-    if (lane == 0) {
-        num = __builtin_fma((double)mn, dn, sd);
-    } else {
-        const double v = __builtin_fma(sq, dn, -(se * se));
-        num = __builtin_sqrt(v > 0.0 ? v : 0.0);
-    }
-    const float r = (float)(num / (1000.0 * dn));
+    // lane 0: avg = (n MIN + sd) / (1000 n), rounded once to f32;
+    // lane 1: std = sqrt(n sq - se^2) / (1000 n) as sqrtf of the f32-rounded variance in us^2
+    //         (f64 quotient, then one f32 rounding and a correctly rounded f32 root: ~1e-7
+    //         relative, inside the FAST bar, without the f64 square-root sequence)
+    const double den = 1000.0 * dn;
+    const double vq = __builtin_fma(sq, dn, -(se * se));
+    const double num = lane == 0 ? __builtin_fma((double)mn, dn, sd) : (vq > 0.0 ? vq : 0.0);
+    const double q = num / (lane == 0 ? den : den * den);
+    const float r = lane == 0 ? (float)q : __builtin_sqrtf((float)q);
     const float avg = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 0));
     const float sdv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 1));
     if (lane == 0) {
