@@ -121,54 +121,8 @@ struct Bins {
     static_assert((1 << LOG) == NB, "NB must be a power of two <= 1024");
 };
 
-// Locate the buckets holding relative ranks ta <= tb in the wave's histogram (one read
-// of the bins).  For each: bucket index, elements in lower buckets, count of the bucket.
-template <int PL>
-__device__ __forceinline__ void hist_locate2(const unsigned* hist, unsigned ta, unsigned tb,
-                                             unsigned& ba, unsigned& bfa, unsigned& ca,
-                                             unsigned& bb, unsigned& bfb, unsigned& cb) {
-    constexpr int BPL = Bins<PL>::BPL;
-    const int lane = lane_id();
-    unsigned h[BPL];
-    unsigned local = 0;
-#pragma unroll
-    for (int j = 0; j < BPL; ++j) {
-        h[j] = hist[lane * BPL + j];
-        local += h[j];
-    }
-    const unsigned incl = wave_incl_scan_u32(local);
-    const unsigned excl = incl - local;
-    // first lane whose range reaches the target (< 64 since target < total)
-    const int La = __popcll(__ballot(incl <= ta));
-    const int Lb = __popcll(__ballot(incl <= tb));
-    unsigned run = excl, sa = 0, pa = 0, na = 0, sb = 0, pb = 0, nb = 0;
-    bool fa = false, fb = false;
-#pragma unroll
-    for (int j = 0; j < BPL; ++j) {
-        const unsigned nxt = run + h[j];
-        if (!fa && nxt > ta) {
-            fa = true;
-            sa = (unsigned)(lane * BPL + j);
-            pa = run;
-            na = h[j];
-        }
-        if (!fb && nxt > tb) {
-            fb = true;
-            sb = (unsigned)(lane * BPL + j);
-            pb = run;
-            nb = h[j];
-        }
-        run = nxt;
-    }
-    ba = __builtin_amdgcn_readlane(sa, La);
-    bfa = __builtin_amdgcn_readlane(pa, La);
-    ca = __builtin_amdgcn_readlane(na, La);
-    bb = __builtin_amdgcn_readlane(sb, Lb);
-    bfb = __builtin_amdgcn_readlane(pb, Lb);
-    cb = __builtin_amdgcn_readlane(nb, Lb);
-}
-
-// One target: bucket holding relative rank ta, elements below it, and its count.
+// Locate the bucket holding relative rank ta in the wave's histogram (one read of the bins):
+// bucket index, elements in lower buckets, count of the bucket.
 template <int PL>
 __device__ __forceinline__ void hist_locate1(const unsigned* hist, unsigned ta, unsigned& ba,
                                              unsigned& bfa, unsigned& ca) {
