@@ -73,10 +73,10 @@ __device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) 
 }
 
 // Epilogue of the FAST kernels, lane-parallel: lanes 0-3 convert MIN, MAX, s[t0], s[t1]
-// in one ns_to_us, lanes 0/1 form avg and std in one f64 divide; lane 0 stores.
+// in one ns_to_us, lanes 0/1 form avg and std from one f64 divide; lane 0 stores.
 //   sd = sum(d), sq = sum((d - c)^2) over the n samples, d = x - MIN.
 //   avg = (n MIN + sd) / (1000 n)               (numerator exact in f64)
-//   std = sqrt(n sq - (sd - n c)^2) / (1000 n)   (population std, CuptiProfiler.cpp:66-70)
+//   std = sqrtf(f32((n sq - (sd - n c)^2) / (1000 n)^2))  (population std, CuptiProfiler.cpp:66-70)
 __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, int n,
                                            unsigned mn, unsigned mx, unsigned d0, unsigned d1,
                                            double sd, double sq, unsigned c, const ColRef& cr) {
