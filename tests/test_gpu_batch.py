@@ -110,17 +110,22 @@ def test_zipf_order_is_a_valid_interleaving():
 
 
 def test_graph_replay_matches_eager():
-    # MatrixReporter.graph: the same kernels captured once and replayed; three successive
-    # reports (history carried) equal the eager reporter's bit for bit
+    # MatrixReporter.graph: the same kernels captured once and replayed; four successive
+    # reports (history carried) equal the eager reporter's bit for bit, whether replayed as one
+    # graph or as the stats / rest halves
     R, K, S, cap = 48, 300, 700, 512
     ns = synth.synth_matrix(R, K, S)
     eager = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
     graphed = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
     g = graphed.graph(ns, S)
     graphed.reset_history()  # the capture's eager warm pass updated the history once
-    for _ in range(3):
+    for i in range(4):  # the one-graph report and the two-graph (timed) halves alternate
         a = eager.report(ns, S)
-        b = g.run()
+        if i % 2 == 0:
+            b = g.run()
+        else:
+            g.run_stats()
+            b = g.run_rest()
         assert np.array_equal(a.gpu_relative, b.gpu_relative)
         assert np.array_equal(a.gpu_individual, b.gpu_individual)
         assert np.array_equal(a.stragglers_relative, b.stragglers_relative)
