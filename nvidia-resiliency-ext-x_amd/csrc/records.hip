@@ -76,15 +76,33 @@ __device__ __forceinline__ void for_records(const nvrx_record* rs, int64_t lo, i
     }
 }
 
+// record pairs [p_lo, p_hi) of a 16-B aligned pair array, f(pair, index) per pair, with the
+// same RB_UNROLL loads in flight per lane as for_records.
+template <class F>
+__device__ __forceinline__ void for_pairs(const u32x4* q, int64_t p_lo, int64_t p_hi, int lane, F&& f) {
+    int64_t i = p_lo + lane;
+    for (; i + 64 * (RB_UNROLL - 1) < p_hi; i += 64 * RB_UNROLL) {
+        u32x4 w[RB_UNROLL];
+#pragma unroll
+        for (int u = 0; u < RB_UNROLL; ++u) w[u] = __builtin_nontemporal_load(q + i + 64 * u);
+#pragma unroll
+        for (int u = 0; u < RB_UNROLL; ++u) f(w[u], i + 64 * u);
+    }
+    for (; i < p_hi; i += 64) f(q[i], i);
+}
+
 template <int RB_WAVES>
 __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
-    int32_t* counts) {
+    int32_t* counts, int64_t stash_pairs) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
     uint32_t* start = lds + 2 * nslots; // [nslots] bucket start (relative to stream base) | RB_OVF
+    // [RB_WAVES][stash_pairs] record pairs: the head of every wave's chunk, kept from pass 1
+    // for pass 2 (which would otherwise re-read them from the memory side)
+    u32x4* stash = (u32x4*)(lds + ((3 * nslots + 3) & ~(int64_t)3));
     __shared__ uint32_t any_ovf;
     __shared__ uint32_t wtot[RB_WAVES];
     const int64_t t = blockIdx.x;
@@ -99,6 +117,10 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     const int64_t per = ((n + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
     const int64_t lo = min(n, per * wave), hi = min(n, lo + per);
     const bool wpairs = pairs && ((hi - lo) % 2 == 0);
+    // pairs of this wave's chunk held in LDS between the passes (0 when not pair-aligned)
+    const int64_t snp = wpairs ? min((hi - lo) >> 1, stash_pairs) : 0;
+    u32x4* wstash = stash + wave * stash_pairs;
+    const u32x4* wq = (const u32x4*)(rs + lo);
 
     for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
         cnt[s] = 0u;
@@ -106,9 +128,15 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     }
     if (threadIdx.x == 0) any_ovf = force_stable ? 1u : 0u;
     __syncthreads();
-    for_records(rs, lo, hi, lane, wpairs, [&](const nvrx_record& r) {
+    const auto count = [&](const nvrx_record& r) {
         if (r.slot < (uint32_t)nslots) atomicAdd(&cnt[r.slot], 1u);
+    };
+    for_pairs(wq, 0, snp, lane, [&](const u32x4& w, int64_t p) {
+        wstash[p] = w;
+        count(nvrx_record{w.x, w.y});
+        count(nvrx_record{w.z, w.w});
     });
+    for_records(rs, lo + 2 * snp, hi, lane, wpairs, count);
     __syncthreads();
 
     // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
@@ -163,12 +191,18 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     // start, so a record costs one returning LDS atomic (a lookup of start[] before the atomic
     // doubled the dependent LDS round trips: 4.5 -> 3.x ms on configs[3]); overflowed slots
     // hold RB_OVF, which the increments keep set, and are skipped here.
-    for_records(rs, lo, hi, lane, wpairs, [&](const nvrx_record& r) {
+    const auto place = [&](const nvrx_record& r) {
         if (r.slot < (uint32_t)nslots) {
             const uint32_t pos = atomicAdd(&cur[r.slot], 1u);
             if (!(pos & RB_OVF)) out[pos] = r.ns;
         }
-    });
+    };
+    for (int64_t p = lane; p < snp; p += 64) {  // the stashed head of the chunk, from LDS
+        const u32x4 w = wstash[p];
+        place(nvrx_record{w.x, w.y});
+        place(nvrx_record{w.z, w.w});
+    }
+    for_records(rs, lo + 2 * snp, hi, lane, wpairs, place);
     if (!any_ovf) return;
     __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
     if (wave != 0) return;
@@ -208,6 +242,10 @@ int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
     return ((n + 3) & ~(int64_t)3) + nstreams * stream_slack(nslots);
 }
 
+// dynamic LDS of a bucketing launch: a single workgroup may take the whole 160 KiB of a CU
+// (MI355X_MICROARCH.md), less the kernel's few static bytes
+constexpr size_t RB_LAUNCH_LDS = 160 * 1024 - 256;
+
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
                           int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st) {
@@ -232,7 +270,7 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     }();
     size_t lds_launch = lds;
     if (bpc > 0) lds_launch = std::max(lds, (size_t)(160 * 1024) / (size_t)bpc - 1024);
-    if (lds_launch > NVRX_RECORDS_MAX_LDS) lds_launch = std::max(lds, (size_t)NVRX_RECORDS_MAX_LDS);
+    if (lds_launch > RB_LAUNCH_LDS) lds_launch = std::max(lds, RB_LAUNCH_LDS);
     const void* fn = waves == 4    ? (const void*)records_bucket_kernel<4>
                      : waves == 8 ? (const void*)records_bucket_kernel<8>
                                   : (const void*)records_bucket_kernel<16>;
@@ -240,20 +278,31 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     const int wi = waves == 4 ? 0 : waves == 8 ? 1 : 2;
     if (!attr_set[wi]) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           NVRX_RECORDS_MAX_LDS);
+                                           (int)RB_LAUNCH_LDS);
         if (e != hipSuccess) return e;
         attr_set[wi] = true;
     }
+    // The LDS that the padding leaves over holds the head of every wave's chunk from pass 1
+    // to pass 2 (a whole number of 64-pair wave loads per wave; NVRX_RB_STASH=0 disables).
+    static const bool use_stash = [] {
+        const char* e = getenv("NVRX_RB_STASH");
+        return !(e && atoi(e) == 0);
+    }();
+    const size_t counters = (size_t)((3 * nslots + 3) & ~(int64_t)3) * sizeof(uint32_t);
+    int64_t stash_pairs = 0;
+    if (use_stash && lds_launch > counters)
+        stash_pairs = (int64_t)((lds_launch - counters) / (16 * (size_t)waves)) & ~(int64_t)63;
+    if (counters + (size_t)waves * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nstreams), block(64 * waves);
     if (waves == 4)
         hipLaunchKernelGGL(records_bucket_kernel<4>, grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts);
+                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs);
     else if (waves == 8)
         hipLaunchKernelGGL(records_bucket_kernel<8>, grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts);
+                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs);
     else
         hipLaunchKernelGGL(records_bucket_kernel<16>, grid, block, lds_launch, st, recs, rec_off,
-                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts);
+                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs);
     return hipGetLastError();
 }
 

@@ -30,7 +30,10 @@ def _streams(rng, nstreams, nslots, lo, hi):
     return np.concatenate(recs), np.array(off, np.int64)
 
 
-@pytest.mark.parametrize("cap,lo,hi", [(8192, 0, 40), (7, 0, 30), (16, 10, 100), (3, 0, 5)])
+# (8192, 500, 2000) / (1000, 500, 2000): ~46k records per stream, longer than the LDS stash of a
+# wave's chunk head (records.hip), so pass 2 reads both the stash and the memory side
+@pytest.mark.parametrize("cap,lo,hi", [(8192, 0, 40), (7, 0, 30), (16, 10, 100), (3, 0, 5),
+                                       (8192, 500, 2000), (1000, 500, 2000)])
 def test_records_bucket_keeps_last_cap_per_slot(cap, lo, hi):
     rng = np.random.default_rng(cap * 7 + hi)
     nstreams, nslots = 5, 37
