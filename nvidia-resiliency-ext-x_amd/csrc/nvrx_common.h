@@ -193,4 +193,5 @@ __device__ __forceinline__ float ns_to_us(unsigned ns) {
 }  // namespace nvrx
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));

@@ -95,7 +95,7 @@ template <int RB_WAVES>
 __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
-    int32_t* counts, int64_t stash_pairs) {
+    int32_t* counts, int64_t stash_pairs, int interleave) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
@@ -197,12 +197,42 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
             if (!(pos & RB_OVF)) out[pos] = r.ns;
         }
     };
-    for (int64_t p = lane; p < snp; p += 64) {  // the stashed head of the chunk, from LDS
-        const u32x4 w = wstash[p];
-        place(nvrx_record{w.x, w.y});
-        place(nvrx_record{w.z, w.w});
+    // The stashed head of the chunk (LDS) is placed while each batch of the rest's loads is
+    // in flight: `per_it` stashed pairs per lane between issuing a batch and consuming it.
+    int64_t sp = lane;  // this lane's stash cursor
+    const auto place_stash = [&](int m) {
+        for (int j = 0; j < m && sp < snp; ++j, sp += 64) {
+            const u32x4 w = wstash[sp];
+            place(nvrx_record{w.x, w.y});
+            place(nvrx_record{w.z, w.w});
+        }
+    };
+    if (snp > 0 && interleave) {
+        const int64_t np = (hi - lo) >> 1;
+        const int64_t iters = (np - snp) / (64 * RB_UNROLL);
+        const int per_it = iters > 0 ? (int)((snp / 64 + iters - 1) / iters) : 0;
+        int64_t i = snp + lane;
+        for (; i + 64 * (RB_UNROLL - 1) < np; i += 64 * RB_UNROLL) {
+            u32x4 w[RB_UNROLL];
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) w[u] = __builtin_nontemporal_load(wq + i + 64 * u);
+            place_stash(per_it);
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) {
+                place(nvrx_record{w[u].x, w[u].y});
+                place(nvrx_record{w[u].z, w[u].w});
+            }
+        }
+        for (; i < np; i += 64) {
+            const u32x4 w = wq[i];
+            place(nvrx_record{w.x, w.y});
+            place(nvrx_record{w.z, w.w});
+        }
+        place_stash(1 << 30);
+    } else {
+        place_stash(1 << 30);
+        for_records(rs, lo + 2 * snp, hi, lane, wpairs, place);
     }
-    for_records(rs, lo + 2 * snp, hi, lane, wpairs, place);
     if (!any_ovf) return;
     __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
     if (wave != 0) return;
@@ -288,6 +318,10 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
         const char* e = getenv("NVRX_RB_STASH");
         return !(e && atoi(e) == 0);
     }();
+    static const int stash_interleave = [] {  // NVRX_RB_STASH=1: stash placed before the rest
+        const char* e = getenv("NVRX_RB_STASH");
+        return (e && atoi(e) == 1) ? 0 : 1;
+    }();
     const size_t counters = (size_t)((3 * nslots + 3) & ~(int64_t)3) * sizeof(uint32_t);
     int64_t stash_pairs = 0;
     if (use_stash && lds_launch > counters)
@@ -296,13 +330,16 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     const dim3 grid((unsigned)nstreams), block(64 * waves);
     if (waves == 4)
         hipLaunchKernelGGL(records_bucket_kernel<4>, grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs);
+                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
+                           stash_interleave);
     else if (waves == 8)
         hipLaunchKernelGGL(records_bucket_kernel<8>, grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs);
+                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
+                           stash_interleave);
     else
         hipLaunchKernelGGL(records_bucket_kernel<16>, grid, block, lds_launch, st, recs, rec_off,
-                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs);
+                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
+                           stash_interleave);
     return hipGetLastError();
 }
 
