@@ -33,6 +33,11 @@ struct RaggedSegs {  // segment s = base[off[s] : off[s] + len[s]] (len NULL: of
         p = base + (e - keep);
         n = (int)keep;
     }
+    // the retained length alone (no offset load when `lens` is given)
+    __device__ __forceinline__ int kept_len(int64_t s) const {
+        const int64_t len = lens ? (int64_t)lens[s] : off[s + 1] - off[s];
+        return (int)((cap > 0 && len > cap) ? cap : len);
+    }
 };
 
 // Optional fused per-column reference (segment s = row s / ncols, column s % ncols):

@@ -35,6 +35,10 @@ enum : int {
 };
 constexpr int CLS_THREADS = 1024;
 constexpr int CLS_MAX_BLOCKS = 1024;
+// segment lengths loaded per thread before any is classified: a block's chunk is tens of
+// thousands of segments, and one dependent load per 1024 of them left both passes
+// latency-bound (configs[3]: 153 + 118 us for 33.5 M segments)
+constexpr int CLS_BATCH = 8;
 
 // need = retained samples + misalignment slack a wave would have to hold
 __device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
@@ -81,21 +85,25 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * chunk;
     const int64_t hi = min(nseg, lo + chunk);
-    for (int64_t b = lo; b < hi; b += CLS_THREADS) {
-        const int64_t s = b + threadIdx.x;
-        int cls = -1;
-        if (s < hi) {
-            const uint32_t* p;
-            int n;
-            segs.get(s, p, n);
-            if (n == 0) {
+    for (int64_t b = lo; b < hi; b += CLS_THREADS * CLS_BATCH) {
+        int n[CLS_BATCH];
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            n[j] = s < hi ? segs.kept_len(s) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            int cls = -1;
+            if (n[j] == 0) {
                 write_empty(out, s);
                 cr.miss(s);
-            } else if (n > 0) {  // n < 0: reduced elsewhere
-                cls = seg_class(n, aligned16 != 0, exact != 0);
+            } else if (n[j] > 0) {  // n < 0: reduced elsewhere (or past the chunk)
+                cls = seg_class(n[j], aligned16 != 0, exact != 0);
             }
+            wave_class_add(lcnt, cls);
         }
-        wave_class_add(lcnt, cls);
     }
     __syncthreads();
     if (threadIdx.x < NCLASS) bcnt[(int64_t)blockIdx.x * NCLASS + threadIdx.x] = lcnt[threadIdx.x];
@@ -141,17 +149,20 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * chunk;
     const int64_t hi = min(nseg, lo + chunk);
-    for (int64_t b = lo; b < hi; b += CLS_THREADS) {
-        const int64_t s = b + threadIdx.x;
-        int cls = -1;
-        if (s < hi) {
-            const uint32_t* p;
-            int n;
-            segs.get(s, p, n);
-            if (n > 0) cls = seg_class(n, aligned16 != 0, exact != 0);
+    for (int64_t b = lo; b < hi; b += CLS_THREADS * CLS_BATCH) {
+        int n[CLS_BATCH];
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            n[j] = s < hi ? segs.kept_len(s) : -1;
         }
-        const uint32_t r = wave_class_add(lcnt, cls);
-        if (cls >= 0) list[lbase[cls] + r] = (uint32_t)s;
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {  // the same order as the counting pass
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            const int cls = n[j] > 0 ? seg_class(n[j], aligned16 != 0, exact != 0) : -1;
+            const uint32_t r = wave_class_add(lcnt, cls);
+            if (cls >= 0) list[lbase[cls] + r] = (uint32_t)s;
+        }
     }
 }
 
