@@ -85,6 +85,11 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * chunk;
     const int64_t hi = min(nseg, lo + chunk);
+    // per-lane class counters in registers (no LDS traffic per segment), one wave reduction
+    // and one LDS add per class at the end
+    unsigned mine[NCLASS];
+#pragma unroll
+    for (int c = 0; c < NCLASS; ++c) mine[c] = 0u;
     for (int64_t b = lo; b < hi; b += CLS_THREADS * CLS_BATCH) {
         int n[CLS_BATCH];
 #pragma unroll
@@ -95,15 +100,20 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
 #pragma unroll
         for (int j = 0; j < CLS_BATCH; ++j) {
             const int64_t s = b + j * CLS_THREADS + threadIdx.x;
-            int cls = -1;
             if (n[j] == 0) {
                 write_empty(out, s);
                 cr.miss(s);
             } else if (n[j] > 0) {  // n < 0: reduced elsewhere (or past the chunk)
-                cls = seg_class(n[j], aligned16 != 0, exact != 0);
+                const int cls = seg_class(n[j], aligned16 != 0, exact != 0);
+#pragma unroll
+                for (int c = 0; c < NCLASS; ++c) mine[c] += cls == c ? 1u : 0u;
             }
-            wave_class_add(lcnt, cls);
         }
+    }
+#pragma unroll
+    for (int c = 0; c < NCLASS; ++c) {
+        const unsigned w = wave_sum_u32(mine[c]);
+        if (lane_id() == 0 && w) atomicAdd(&lcnt[c], w);
     }
     __syncthreads();
     if (threadIdx.x < NCLASS) bcnt[(int64_t)blockIdx.x * NCLASS + threadIdx.x] = lcnt[threadIdx.x];
