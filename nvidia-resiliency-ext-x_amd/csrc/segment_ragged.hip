@@ -182,35 +182,58 @@ struct LaneOcc {
     static constexpr int W = N >= 128 ? 2 : N >= 64 ? 4 : N >= 32 ? 6 : 8;
 };
 
+// Segments per lane per step: each takes a chain of three dependent loads (list entry,
+// descriptor, samples), so the shortest class runs B chains side by side.
+template <int N>
+struct LaneBatch {
+    static constexpr int B = N <= 8 ? 4 : 1;  // 2 for N = 32: 189 -> 214 us (configs[3])
+};
+
 // One lane per segment of 1..N samples.  u32 -> f32 us is monotone, so sorting the
 // integer ns sorts the floats computeStats sorts; then CuptiProfiler.cpp:53-71.
 template <int N>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LaneOcc<N>::W)))
 void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
                            int aligned16, nvrx_stats_soa out, ColRef cr) {
+    constexpr int B = LaneBatch<N>::B;
+    // 32-bit list indices (a 64-bit loop cost lane<8> 315 -> 372 us); the host keeps the
+    // segment count below 2^32 - 2^26, so i + B * G never wraps
     const uint32_t start = cls[0], cnt = cls[1];
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += gridDim.x * 256u) {
-        const int64_t s = list[start + i];
-        const uint32_t* p;
-        int n;
-        segs.get(s, p, n);  // 1 <= n <= N
-        unsigned v[N];
-        if (aligned16) {
-            const u32x4* q = (const u32x4*)p;
+    const uint32_t G = gridDim.x * 256u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += B * G) {
+        int64_t s[B];
+        const uint32_t* p[B];
+        int n[B];
 #pragma unroll
-            for (int j = 0; j < N / 4; ++j) {
-                u32x4 w = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-                if (4 * j < n) w = q[j];
-                v[4 * j + 0] = w.x;
-                v[4 * j + 1] = w.y;
-                v[4 * j + 2] = w.z;
-                v[4 * j + 3] = w.w;
-            }
-        } else {
+        for (int b = 0; b < B; ++b) s[b] = i + b * G < cnt ? (int64_t)list[start + i + b * G] : -1;
 #pragma unroll
-            for (int j = 0; j < N; ++j) v[j] = j < n ? p[j] : 0xFFFFFFFFu;
+        for (int b = 0; b < B; ++b) {
+            n[b] = 0;
+            p[b] = nullptr;
+            if (s[b] >= 0) segs.get(s[b], p[b], n[b]);  // 1 <= n <= N
         }
-        lane_stats<N>(v, n, s, out, cr);
+        unsigned v[B][N];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (aligned16) {
+                const u32x4* q = (const u32x4*)p[b];
+#pragma unroll
+                for (int j = 0; j < N / 4; ++j) {
+                    u32x4 w = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+                    if (4 * j < n[b]) w = q[j];
+                    v[b][4 * j + 0] = w.x;
+                    v[b][4 * j + 1] = w.y;
+                    v[b][4 * j + 2] = w.z;
+                    v[b][4 * j + 3] = w.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) v[b][j] = j < n[b] ? p[b][j] : 0xFFFFFFFFu;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (s[b] >= 0) lane_stats<N>(v[b], n[b], s[b], out, cr);
     }
 }
 
@@ -394,7 +417,7 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
     const int64_t need = aligned16 ? keep : keep + 3;
     const bool exact = mode == NVRX_STATS_EXACT;
-    if (nseg >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    if (nseg >= ((int64_t)1 << 32) - ((int64_t)1 << 26)) return hipErrorInvalidValue;  // 32-bit lists
 
     const int64_t nblocks = std::min<int64_t>(CLS_MAX_BLOCKS, (nseg + CLS_THREADS - 1) / CLS_THREADS);
     const int64_t chunk = (nseg + nblocks - 1) / nblocks;
