@@ -1,30 +1,35 @@
 """CPU: host-side logic of the scoring path that involves no device -- the report interval
 tracker (reference tests/straggler/unit/test_interval_tracker.py), name-id agreement across
 ranks (name_mapper.py:56-81) and the dist_utils collectives, on gloo worlds."""
-import time
 
 import pytest
 
 from _mp import run_world
 
 
-def test_interval_estimate_single_process():
+def test_interval_estimate_single_process(monkeypatch):
+    # a fake monotonic clock in exact binary steps (1/64 s), so the estimate is exact and
+    # the test does not depend on how long sleeps take on a loaded host
+    from types import SimpleNamespace
+
     from nvidia_resiliency_ext.straggler import interval_tracker
 
+    clock = SimpleNamespace(t=1000.0)
+    monkeypatch.setattr(interval_tracker, "time", SimpleNamespace(monotonic=lambda: clock.t))
     tr = interval_tracker.ReportIntervalTracker()
     tr.time_interval = 0.5
     assert tr.iter_interval is None
     for i in range(120):
         tr.iter_increase()
-        time.sleep(0.01)
+        clock.t += 1 / 64
         if tr.current_iter <= tr.INTERVAL_ESTIMATION_ITERS:
             assert tr.iter_interval is None
         else:
             assert tr.is_interval_elapsed() == (tr.current_iter % tr.iter_interval == 0)
         if i < tr.INTERVAL_ESTIMATION_ITERS // 2:
-            time.sleep(0.04)  # slow warm-up steps do not move the (lower) median
+            clock.t += 4 / 64  # slow warm-up steps do not move the (lower) median
     assert not tr.step_times
-    assert abs(tr.iter_interval - 50) < 5
+    assert tr.iter_interval == 32  # 0.5 s / (1/64 s)
 
 
 def test_interval_never_below_profiling_interval():
