@@ -16,13 +16,20 @@ simulated ranks (47,482 {slot, ns} records per rank, kernel k pushed floor(8192/
 times, 1.3x stragglers) -> bucket by slot -> length-classed stats -> scores.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-(N > 1: launched by torch.distributed.run, one process per GPU.)
+N > 1: one process per GPU over RCCL.  Under torchrun (WORLD_SIZE set) every process is one
+rank; run directly with --gpus N > 1, this script starts `torch.distributed.run
+--nproc-per-node N` on itself as a CHILD process (before anything touches the GPU) and exits
+with its status.  NVRX_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with every rank on
+GPU 0 and the partials exchanged over gloo (never a reported number); --dry-run: the launcher
+and rendezvous only (no GPU work; CPU test of the launcher).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,7 +54,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup():
+def launch_ranks(nproc: int) -> int:
+    """Start `torch.distributed.run` with nproc ranks of this script as a child process (no
+    exec: nothing in this process has touched the GPU, and it only waits) and return its exit
+    status.  Rendezvous on 127.0.0.1 with a free port."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching:", " ".join(cmd))
+    return subprocess.call(cmd)
+
+
+def dist_setup(dry_run=False):
     """One process per GPU over RCCL.  NVRX_BENCH_BACKEND=gloo is a rehearsal mode only:
     every rank on GPU (LOCAL_RANK mod the visible GPUs), partials exchanged over gloo --
     the multi-rank code path of this script on a one-GPU box; never a reported number."""
@@ -55,6 +76,10 @@ def dist_setup():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("NVRX_BENCH_BACKEND", "nccl")
+    if dry_run:  # rendezvous only, on the CPU
+        if world > 1:
+            torch.distributed.init_process_group("gloo")
+        return rank, world, torch.device("cpu")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -174,7 +199,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
         h = recs[:cpu_ranks * N].cpu().numpy().view(np.uint32)
         off = np.arange(cpu_ranks + 1, dtype=np.int64) * N
         t1 = time.perf_counter()
-        st = O.records_stats(h, off, K, cap=cap, nthreads=threads)
+        st = O.records_stats(h, off, K, cap=cap, nthreads=threads, route="baseline")
         gr, gi = O.scores(st["num"].reshape(cpu_ranks, K), st["med"].reshape(cpu_ranks, K),
                           st["avg"].reshape(cpu_ranks, K))
         O.stragglers(gr, THR)
@@ -185,9 +210,21 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
                      for f in ("num", "min", "max", "med"))
         out["cpu_baseline"] = dict(value=cpu_ranks * N / dt, unit="records/s", cores=threads,
                                    kind="port", sample=f"{cpu_ranks} of {R} ranks ({cpu_ranks * N} "
-                                   f"records, {dt:.2f} s): oracle C ring-push + computeStats + "
-                                   f"scoring restatement", gpu_stats_bit_exact_on_sample=parity)
+                                   f"records, {dt:.2f} s): per-record ring pushes + std::sort "
+                                   f"computeStats (oracle/baseline.cpp) + scoring restatement",
+                                   gpu_stats_bit_exact_on_sample=parity)
     return out
+
+
+def cpu_threads() -> int:
+    """Host threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, 16 on the GPU
+    boxes), never more than this process may run on."""
+    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    return max(1, min(t, len(os.sched_getaffinity(0))))
+
+
+def comm_max(x: float, world: int, dev) -> float:
+    return allreduce(x, torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
 
 
 def pmc_traffic(workload: str):
@@ -204,9 +241,12 @@ def pmc_traffic(workload: str):
 
 
 def cpu_baseline(ns, kidx, cfg, res_gpu_stats, sample_ranks, threads):
-    """Host-CPU Reporter (the oracle's C restatement of computeStats + scoring), threaded
-    over `threads` host cores, on the first `sample_ranks` ranks of the same workload;
-    also spot-checks the GPU stats of those ranks bit for bit."""
+    """Host-CPU Reporter on the first `sample_ranks` ranks of the same workload, threaded over
+    `threads` host cores: the reference's per-kernel path restated in C++ (oracle/baseline.cpp:
+    every pushed duration through a ring of the last cap, then computeStats with std::sort --
+    within a few % of the reference's own code compiled from its sources, per core,
+    profiles/r02/cpu_baseline_validation.json) + the C restatement of the scoring.  Also
+    checks the GPU stats of those ranks bit for bit."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -214,7 +254,7 @@ def cpu_baseline(ns, kidx, cfg, res_gpu_stats, sample_ranks, threads):
     K = len(kidx)
     host = ns[:R].contiguous().cpu().numpy().view(np.uint32).reshape(-1)
     t0 = time.perf_counter()
-    st = O.matrix_stats(host, R * K, s_push, 0, s_push, cap, nthreads=threads)
+    st = O.matrix_stats(host, R * K, s_push, 0, s_push, cap, nthreads=threads, route="baseline")
     num = st["num"].reshape(R, K)
     med = st["med"].reshape(R, K)
     avg = st["avg"].reshape(R, K)
@@ -239,13 +279,27 @@ def main():
     ap.add_argument("--no-latency4096", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-ranks", type=int, default=16)
+    ap.add_argument("--cpu4096-ranks", type=int, default=128)
     ap.add_argument("--no-zipf", action="store_true")
     ap.add_argument("--zipf-cpu-ranks", type=int, default=1024)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
+    ap.add_argument("--dry-run", action="store_true", help="launcher + rendezvous only (no GPU)")
     args = ap.parse_args()
-    rank, world, dev = dist_setup()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    rank, world, dev = dist_setup(args.dry_run)
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    backend = torch.distributed.get_backend() if world > 1 else None
+    if args.dry_run:
+        if world > 1:
+            torch.distributed.barrier()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": world,
+                              "backend": backend}), flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
 
     # ---------------- value: configs[1] per GPU, kernel-hash sharded (weak) ----------
     K_global = C2["K"] * world
@@ -257,7 +311,8 @@ def main():
     ms_per_step = tmax / args.steps * 1e3
     # roofline of the dominant kernel (segment stats) on this GPU
     alg_bytes = 4 * r["samples"] + STATS_BYTES_PER_SEGMENT * r["nseg"]
-    achieved = alg_bytes / (r["kern_ms"] * 1e-3)
+    kern_ms = comm_max(r["kern_ms"], world, dev)  # the slowest rank's stats kernel
+    achieved = alg_bytes / (kern_ms * 1e-3)
     res = r["res"]
     strag_true = synth.straggler_ranks(C2["R"])
     sets_ok = bool(np.array_equal(res.stragglers_relative, strag_true.astype(bool)))
@@ -274,17 +329,30 @@ def main():
                          world, dev)
         n4 = max(3, args.steps // 4)
         s4 = r4["res"]
+        k4 = comm_max(r4["kern_ms"], world, dev)
         lat = dict(ranks=C3["R"], kernels=C3["K"], samples_per_kernel=C3["s_push"],
                    ms_per_report=t4 / n4 * 1e3, samples_per_s=tot4 * n4 / t4,
-                   stats_kernel_ms=r4["kern_ms"],
-                   stats_kernel_hbm_frac=(4 * r4["samples"] + 24 * r4["nseg"]) / (r4["kern_ms"] * 1e-3) / HBM_PEAK,
+                   stats_kernel_ms=k4,
+                   stats_kernel_hbm_frac=(4 * r4["samples"] + 24 * r4["nseg"]) / (k4 * 1e-3) / HBM_PEAK,
                    straggler_sets_exact=bool(np.array_equal(
                        s4.stragglers_relative, synth.straggler_ranks(C3["R"]).astype(bool))))
+        if world == 1 and rank == 0 and not args.no_cpu_baseline:
+            # the north_star's >= 100x target is stated at this configuration
+            cb4 = cpu_baseline(r4["ns"], r4["kidx"], C3, r4["rep"].stats, args.cpu4096_ranks,
+                               cpu_threads())
+            lat["cpu_baseline"] = dict(
+                value=cb4["value"], unit="samples/s", cores=cpu_threads(), kind="port",
+                per_core=cb4["value"] / cpu_threads(),
+                sample=f"{args.cpu4096_ranks} of 4096 ranks x 2048 kernels x 1024 samples "
+                       f"({cb4['samples']:.3g} samples, {cb4['seconds']:.2f} s): ring pushes + "
+                       f"std::sort computeStats (oracle/baseline.cpp) + scoring restatement",
+                gpu_stats_bit_exact_on_sample=cb4["parity"],
+                cpu_report_ms_extrapolated=4096 * 2048 * 1024 / cb4["value"] * 1e3)
+            lat["gpu_over_cpu"] = lat["samples_per_s"] / cb4["value"]
         del r4
         torch.cuda.empty_cache()
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    threads = cpu_threads()
     # ---------------- configs[3]: Zipf record streams at 16k ranks --------------------
     zipf = None
     if not args.no_zipf:
@@ -309,7 +377,7 @@ def main():
         reps1 = 20
         for _ in range(reps1):
             st1 = O.matrix_stats(host, C1["R"] * C1["K"], C1["s_push"], 0, C1["s_push"], C1["cap"],
-                                 nthreads=min(8, threads))
+                                 nthreads=min(8, threads), route="baseline")
             gr1, _ = O.scores(st1["num"].reshape(C1["R"], C1["K"]), st1["med"].reshape(C1["R"], C1["K"]),
                               st1["avg"].reshape(C1["R"], C1["K"]))
             O.stragglers(gr1, THR)
@@ -329,9 +397,11 @@ def main():
         rep.compute_stats(ns_c2, C2["s_push"])
         cb = cpu_baseline(ns_c2, kidx, C2, rep.stats, args.cpu_sample_ranks, threads)
         cpu = dict(value=cb["value"], unit="samples/s", cores=threads, kind="port",
-                   sample=f"{args.cpu_sample_ranks} of 64 ranks x 2048 kernels x 8192 retained "
-                          f"samples ({cb['samples']:.3g} samples, {cb['seconds']:.2f} s): oracle C "
-                          f"computeStats + scoring restatement",
+                   per_core=cb["value"] / threads,
+                   sample=f"{args.cpu_sample_ranks} of 64 ranks x 2048 kernels x 10000 pushed "
+                          f"(8192 kept; {cb['samples']:.3g} samples, {cb['seconds']:.2f} s): ring "
+                          f"pushes + std::sort computeStats (oracle/baseline.cpp) + scoring "
+                          f"restatement",
                    gpu_stats_bit_exact_on_sample=cb["parity"])
 
     if rank == 0:
@@ -357,12 +427,13 @@ def main():
                        "ranks": C2["R"], "kernels_per_gpu": C2["K"], "kernels_total": K_global,
                        "samples_pushed": C2["s_push"], "ring_cap": C2["cap"],
                        "parallelism": f"kernel-hash shards x{world}" if world > 1 else "1 GPU",
+                       "world_size": world, "backend": backend or "none (1 GPU)",
                        "stats_mode": "fast", "launch": "eager" if args.no_graph else "hip_graph"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic,
                          "kernel": "seg_stats_lean_kernel<128>",
-                         "kernel_ms": r["kern_ms"],
+                         "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,

@@ -1,0 +1,131 @@
+// baseline.cpp -- TEST INFRASTRUCTURE ONLY (linked into oracle/liboracle.so).
+//
+// The timed host-CPU Reporter of bench.py (cpu_baseline.kind = "port"): the reference's
+// per-kernel statistics path restated in C++ the way the reference itself runs it, so that the
+// baseline costs what the reference costs on the same cores --
+//   * every pushed duration converted as bufferCompleted does (CuptiProfiler.cpp:187) and kept
+//     in a per-kernel ring of the last `cap` values (CircularBuffer.h:53-69);
+//   * getStats: linearize, then computeStats (CuptiProfiler.cpp:44-74): a copy, std::sort of the
+//     floats, min / max / median, sequential f32 sums for avg and std.
+// The checker route (nvrx_oracle.c, radix-sorted integer keys) gives identical statistics; this
+// one exists only to be timed (tests/test_oracle_semantics.py checks the two agree).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <numeric>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Stats {
+    int32_t num;
+    float mn, mx, med, avg, sd;
+};
+
+// CuptiProfiler.cpp:44-74, statement by statement
+Stats compute_stats(const std::vector<float>& data) {
+    Stats s{0, NAN, NAN, NAN, NAN, NAN};
+    if (data.empty()) return s;
+    std::vector<float> v(data);
+    std::sort(v.begin(), v.end());
+    const size_t n = v.size();
+    s.mn = v.front();
+    s.mx = v.back();
+    s.med = n % 2 == 0 ? (v[n / 2 - 1] + v[n / 2]) / 2 : v[n / 2];
+    const float sum = std::accumulate(v.begin(), v.end(), 0.0f);
+    s.avg = sum / (float)n;
+    float sq = 0.0f;
+    for (float x : v) sq = sq + (x - s.avg) * (x - s.avg);
+    s.sd = std::sqrt(sq / (float)n);
+    s.num = (int32_t)n;
+    return s;
+}
+
+// a ring of the last cap pushes, linearized oldest first (CircularBuffer.h:53-69)
+struct Ring {
+    std::vector<float> buf;
+    size_t cap, head = 0, size = 0;
+    explicit Ring(size_t c) : buf(c), cap(c) {}
+    void push(float x) {
+        buf[head] = x;
+        head = (head + 1) % cap;
+        if (size < cap) ++size;
+    }
+    std::vector<float> linearize() const {
+        std::vector<float> out(size);
+        const size_t first = (head + cap - size) % cap;
+        for (size_t i = 0; i < size; ++i) out[i] = buf[(first + i) % cap];
+        return out;
+    }
+};
+
+}  // namespace
+
+extern "C" void oracle_baseline_matrix_stats(const uint32_t* ns, int64_t nseg, int64_t stride,
+                                             int64_t begin, int64_t len, int64_t cap, int32_t* num,
+                                             float* mn, float* mx, float* med, float* avg,
+                                             float* sd, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) {
+        th.emplace_back([=] {
+            const int64_t lo = nseg * t / nthreads, hi = nseg * (t + 1) / nthreads;
+            for (int64_t s = lo; s < hi; ++s) {
+                Ring ring((size_t)(cap > 0 ? cap : (len > 0 ? len : 1)));
+                const uint32_t* p = ns + s * stride + begin;
+                for (int64_t i = 0; i < len; ++i) {
+                    const uint64_t start = 0, end = p[i];
+                    ring.push((float)(end - start) / 1000.0f);  // CuptiProfiler.cpp:187
+                }
+                const Stats k = compute_stats(ring.linearize());
+                num[s] = k.num;
+                mn[s] = k.mn;
+                mx[s] = k.mx;
+                med[s] = k.med;
+                avg[s] = k.avg;
+                sd[s] = k.sd;
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+}
+
+// Record streams (configs[3]): per stream t, every {slot, ns} record pushed into its slot's ring
+// in push order (bufferCompleted, CuptiProfiler.cpp:189-198, minus the snprintf'd string key:
+// records carry the slot), then getStats over the slots: out[t * nslots + s].
+extern "C" void oracle_baseline_records_stats(const uint32_t* recs, const int64_t* rec_off,
+                                              int64_t nstreams, int64_t nslots, int64_t cap,
+                                              int32_t* num, float* mn, float* mx, float* med,
+                                              float* avg, float* sd, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) {
+        th.emplace_back([=] {
+            const int64_t lo = nstreams * t / nthreads, hi = nstreams * (t + 1) / nthreads;
+            for (int64_t st = lo; st < hi; ++st) {
+                std::vector<Ring> rings(nslots, Ring((size_t)(cap > 0 ? cap : 1 << 20)));
+                const uint32_t* r = recs + 2 * rec_off[st];
+                const int64_t n = rec_off[st + 1] - rec_off[st];
+                for (int64_t i = 0; i < n; ++i) {
+                    const uint32_t s = r[2 * i];
+                    if (s >= (uint32_t)nslots) continue;
+                    const uint64_t start = 0, end = r[2 * i + 1];
+                    rings[s].push((float)(end - start) / 1000.0f);
+                }
+                for (int64_t s = 0; s < nslots; ++s) {
+                    const Stats k = compute_stats(rings[s].linearize());
+                    const int64_t g = st * nslots + s;
+                    num[g] = k.num;
+                    mn[g] = k.mn;
+                    mx[g] = k.mx;
+                    med[g] = k.med;
+                    avg[g] = k.avg;
+                    sd[g] = k.sd;
+                }
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+}

@@ -38,8 +38,8 @@ class KStats(ctypes.Structure):
 
 def build() -> str:
     """Compile liboracle.so (gcc) if missing or stale."""
-    src = os.path.join(_HERE, "nvrx_oracle.c")
-    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("nvrx_oracle.c", "baseline.cpp")]
+    if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < max(map(os.path.getmtime, srcs)):
         subprocess.check_call(["make", "-s", "-C", _HERE, "all"])
     return _LIB_PATH
 
@@ -65,6 +65,12 @@ def lib():
         L.oracle_ring_linearize.restype = i64
         L.oracle_ring_linearize.argtypes = [P, i64, i64, P]
         L.oracle_matrix_stats.argtypes = [P, i64, i64, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
+        L.oracle_matrix_stats_route.argtypes = [P, i64, i64, i64, i64, i64, P, P, P, P, P, P,
+                                                ctypes.c_int, ctypes.c_int]
+        L.oracle_baseline_matrix_stats.argtypes = [P, i64, i64, i64, i64, i64, P, P, P, P, P, P,
+                                                   ctypes.c_int]
+        L.oracle_baseline_records_stats.argtypes = [P, P, i64, i64, i64, P, P, P, P, P, P,
+                                                    ctypes.c_int]
         L.oracle_records_stats.argtypes = [P, P, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
         L.oracle_kernel_ref.argtypes = [P, P, i64, i64, P]
         L.oracle_scores.argtypes = [P, P, P, i64, i64, P, P, P, P, P]
@@ -125,8 +131,13 @@ def ring_linearize(pushed_f32, cap: int) -> np.ndarray:
 
 
 def matrix_stats(ns: np.ndarray, nseg: int, seg_stride: int, seg_begin: int, seg_len: int,
-                 cap: int = 0, nthreads: int = 1) -> dict:
-    """Stats of segments ns.flat[s*seg_stride+seg_begin : +seg_len], last `cap` kept."""
+                 cap: int = 0, nthreads: int = 1, route: str = "radix") -> dict:
+    """Stats of segments ns.flat[s*seg_stride+seg_begin : +seg_len], last `cap` kept.
+    route "radix": integer keys radix-sorted, then converted (fast; the checker's default);
+    "qsort": converted, then a comparison sort of the floats as computeStats does;
+    "baseline": every sample pushed through a ring, then std::sort computeStats (baseline.cpp,
+    what bench.py times as the host-CPU Reporter).  All give the same sorted float array,
+    hence identical statistics (tests/test_oracle_semantics.py)."""
     ns = np.ascontiguousarray(ns, dtype=np.uint32)
     out = {
         "num": np.empty(nseg, np.int32),
@@ -136,22 +147,33 @@ def matrix_stats(ns: np.ndarray, nseg: int, seg_stride: int, seg_begin: int, seg
         "avg": np.empty(nseg, np.float32),
         "std": np.empty(nseg, np.float32),
     }
-    lib().oracle_matrix_stats(_p(ns), nseg, seg_stride, seg_begin, seg_len, cap,
-                              _p(out["num"]), _p(out["min"]), _p(out["max"]), _p(out["med"]),
-                              _p(out["avg"]), _p(out["std"]), int(nthreads))
+    assert route in ("radix", "qsort", "baseline"), route
+    if route == "baseline":  # baseline.cpp: ring pushes + std::sort computeStats (timed)
+        lib().oracle_baseline_matrix_stats(_p(ns), nseg, seg_stride, seg_begin, seg_len, cap,
+                                           _p(out["num"]), _p(out["min"]), _p(out["max"]),
+                                           _p(out["med"]), _p(out["avg"]), _p(out["std"]),
+                                           int(nthreads))
+        return out
+    lib().oracle_matrix_stats_route(_p(ns), nseg, seg_stride, seg_begin, seg_len, cap,
+                                    _p(out["num"]), _p(out["min"]), _p(out["max"]), _p(out["med"]),
+                                    _p(out["avg"]), _p(out["std"]), int(nthreads),
+                                    1 if route == "qsort" else 0)
     return out
 
 
 def records_stats(recs: np.ndarray, rec_off: np.ndarray, nslots: int, cap: int = 0,
-                  nthreads: int = 1) -> dict:
+                  nthreads: int = 1, route: str = "radix") -> dict:
     """Stats of every (stream, slot) of push-ordered {slot, ns} record streams
-    (CuptiProfiler.cpp:168-203 ring pushes + getStats), out[t*nslots + s]."""
+    (CuptiProfiler.cpp:168-203 ring pushes + getStats), out[t*nslots + s].  route "baseline":
+    per-record ring pushes + std::sort computeStats (baseline.cpp; what bench.py times)."""
     recs = np.ascontiguousarray(recs, dtype=np.uint32).reshape(-1, 2)
     rec_off = np.ascontiguousarray(rec_off, dtype=np.int64)
     nseg = (rec_off.size - 1) * nslots
     out = {k: np.empty(nseg, np.int32 if k == "num" else np.float32)
            for k in ("num", "min", "max", "med", "avg", "std")}
-    lib().oracle_records_stats(_p(recs), _p(rec_off), rec_off.size - 1, nslots, cap,
+    assert route in ("radix", "baseline"), route
+    fn = lib().oracle_baseline_records_stats if route == "baseline" else lib().oracle_records_stats
+    fn(_p(recs), _p(rec_off), rec_off.size - 1, nslots, cap,
                                _p(out["num"]), _p(out["min"]), _p(out["max"]), _p(out["med"]),
                                _p(out["avg"]), _p(out["std"]), int(nthreads))
     return out

@@ -59,4 +59,38 @@ void ref_ns_to_us_array(const uint32_t* ns, int64_t n, float* out) {
         out[i] = duration;
     }
 }
+
+// The reference's per-kernel path over a matrix of integer-ns durations, segment s =
+// ns[s*stride + begin : +len], threaded over segments: every duration converted as
+// bufferCompleted does (CuptiProfiler.cpp:187) and pushed into that kernel's
+// CircularBuffer<float>(cap) (:189-198), then getStats' linearize + computeStats (:140-144).
+// bench.py times this as the host-CPU baseline (cpu_baseline.kind = "reference").
+void ref_matrix_stats(const uint32_t* ns, int64_t nseg, int64_t stride, int64_t begin, int64_t len,
+                      int64_t cap, int32_t* num, float* mn, float* mx, float* med, float* avg,
+                      float* sd, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) {
+        th.emplace_back([=] {
+            const int64_t lo = nseg * t / nthreads, hi = nseg * (t + 1) / nthreads;
+            for (int64_t s = lo; s < hi; ++s) {
+                CircularBuffer<float> rb((size_t)cap);
+                const uint32_t* p = ns + s * stride + begin;
+                for (int64_t i = 0; i < len; ++i) {
+                    const uint64_t start = 0, end = p[i];
+                    const float duration = (end - start) / 1000.0f;
+                    rb.push_back(duration);
+                }
+                const KernelStats k = computeStats(rb.linearize());
+                num[s] = k.num_calls;
+                mn[s] = k.min;
+                mx[s] = k.max;
+                med[s] = k.median;
+                avg[s] = k.avg;
+                sd[s] = k.stddev;
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+}
 }

@@ -1,0 +1,45 @@
+"""bench.py's multi-rank launcher: `python bench.py --gpus N` (no WORLD_SIZE) starts
+torch.distributed.run with N ranks of itself as a child process, and rank 0 prints the one JSON
+line with n_gpus = N (VERDICT r01 "next 2").
+
+CPU: --dry-run (launcher + gloo rendezvous, no GPU work).  GPU: the real 2-rank rehearsal on the
+box's one GPU with the partials exchanged over gloo (NVRX_BENCH_BACKEND=gloo), a reduced run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, timeout):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["NVRX_BENCH_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, env=env,
+                       timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+def test_launcher_two_ranks_dry_run():
+    line = _run(["--gpus", "2", "--dry-run"], timeout=240)
+    assert line == {"dry_run": True, "n_gpus": 2, "world_size": 2, "backend": "gloo"}
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_launcher_two_ranks_gloo_rehearsal():
+    line = _run(["--gpus", "2", "--steps", "3", "--warmup", "1", "--no-zipf", "--no-cpu-baseline"],
+                timeout=380)
+    assert line["n_gpus"] == 2
+    assert line["config"]["world_size"] == 2 and line["config"]["backend"] == "gloo"
+    assert line["config"]["kernels_total"] == 4096
+    assert line["straggler_sets_exact"] is True
+    assert line["latency_4096_ranks"]["straggler_sets_exact"] is True
+    assert 0 < line["roofline"]["frac"] < 1.5

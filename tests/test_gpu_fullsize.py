@@ -1,12 +1,25 @@
-"""GPU: the bench's full-size configurations through size-independent properties:
-configs[1] (64 ranks x 2048 kernels x 10,000 pushed, 8192 kept) and configs[2] (4096 x 2048 x
-1024) at their real sizes --
+"""GPU: full-size parity of the benchmarked configurations against the oracle, over the WHOLE
+simulated world (VERDICT r01 "next 1"):
 
-  * a sample of whole rank rows bit for bit against the oracle's computeStats restatement;
-  * permutation invariance: reversing every retained window leaves NUM/MIN/MAX/MED/AVG bit for
-    bit unchanged and STD within the FAST bar (computeStats sorts; the order is free);
-  * the straggler set equals the generator's injected set (1.3x ranks, threshold 0.8).
+  configs[0] shape  8 ranks x 200 kernels x 1000 samples
+  configs[1]        64 ranks x 2048 kernels x 10,000 pushed (last 8192 kept)
+  configs[2]        4096 ranks x 2048 kernels x 1024
+  configs[3]        16,384 Zipf record streams (47,482 {slot, ns} records each)
+
+For every configuration and two successive reports (the second on fresh samples of another seed,
+so the individual-score history -- reporting.py:298-314 -- carries a real minimum across
+reports):
+  * NUM / MIN / MAX / MED of EVERY (rank, kernel) segment bit for bit against the oracle's
+    ring + computeStats restatement (CuptiProfiler.cpp:44-74, CircularBuffer.h:53-69);
+  * FAST-mode relative and individual GPU scores within 1e-6 relative of the oracle's scores
+    computed from the oracle's own statistics (sequential-f32 AVG/STD as the reference,
+    reporting.py:219-253) -- the max error is printed;
+  * straggler sets (threshold 0.8) equal to the ORACLE's sets and to the injected 1.3x ranks.
+Plus the size-independent checks: reversing every retained window (or record stream) leaves the
+statistics unchanged (computeStats sorts; push order is free when no ring overflows).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -16,109 +29,145 @@ from nvidia_resiliency_ext.straggler import batch, synth
 
 pytestmark = pytest.mark.gpu
 
-EXACT_FIELDS = ("num", "min", "max", "med", "avg")
+SCORE_RTOL = 1e-6  # north_star: scores within 1e-6 relative
+THR = 0.8
+EXACT_FIELDS = ("num", "min", "max", "med")
+THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16),
+                     len(os.sched_getaffinity(0))))
 
 
 def _stats_host(rep):
-    return {f: getattr(rep.stats, f).cpu().numpy() for f in EXACT_FIELDS + ("std",)}
+    return {f: getattr(rep.stats, f).cpu().numpy() for f in ("num", "min", "max", "med", "avg", "std")}
 
 
-def _check_mean_std(kept, g, idx):
-    # FAST mode: AVG / STD are the exact mean / population std of the retained durations
-    # rounded once to f32 -- the reference's sequential f32 sums drift ~1e-5
-    # from them at n = 8192, so the bar is against the exact values, not the oracle's
-    x = kept.astype(np.float64) / 1000.0
-    mean = x.mean(axis=1)
-    std = np.sqrt(((x - mean[:, None]) ** 2).mean(axis=1))
-    np.testing.assert_allclose(g["avg"][idx], mean, rtol=2.5e-7, atol=0)
-    np.testing.assert_allclose(g["std"][idx], std, rtol=1e-6, atol=0)
+def _matrix_oracle_stats(ns, R, K, S, cap, chunk_ranks):
+    """The oracle's statistics of every segment of a device matrix ns[R][K][S], copied to the
+    host a chunk of ranks at a time (pinned staging buffer)."""
+    out = {f: np.empty(R * K, np.int32 if f == "num" else np.float32)
+           for f in ("num", "min", "max", "med", "avg", "std")}
+    stage = torch.empty((min(chunk_ranks, R), K, S), dtype=torch.int32, pin_memory=True)
+    for r0 in range(0, R, chunk_ranks):
+        r1 = min(R, r0 + chunk_ranks)
+        h = stage[:r1 - r0]
+        h.copy_(ns[r0:r1], non_blocking=True)
+        torch.cuda.synchronize()
+        st = O.matrix_stats(h.numpy().view(np.uint32).reshape(-1), (r1 - r0) * K, S, 0, S, cap,
+                            nthreads=THREADS)
+        for f in out:
+            out[f][r0 * K:r1 * K] = st[f]
+    return out
 
 
-def _check_permutation(R, K, S, cap):
-    ns = synth.synth_matrix(R, K, S)
-    rep = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
-    res = rep.report(ns, S)
-    a = _stats_host(rep)
-    assert np.array_equal(res.stragglers_relative, synth.straggler_ranks(R).astype(bool))
-    keep = min(S, cap)
-    flat = ns.view(R * K, S)
-    rev = torch.cat([flat[:, :S - keep], torch.flip(flat[:, S - keep:], dims=[1])], dim=1)
-    del flat
-    rep2 = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
-    res2 = rep2.report(rev.view(R, K, S), S)
-    b = _stats_host(rep2)
+def _check_report(tag, R, K, g, ref, res, hist):
+    """GPU stats g + batch result res vs the oracle statistics ref; hist ([R][K] f64) is the
+    oracle's individual history, updated here (reporting.py:469-474)."""
     for f in EXACT_FIELDS:
-        assert np.array_equal(a[f].view(np.uint32), b[f].view(np.uint32)), f
-    np.testing.assert_allclose(b["std"], a["std"], rtol=2.5e-7, atol=0)
-    np.testing.assert_allclose(res2.gpu_relative, res.gpu_relative, rtol=1e-12)
-    return ns, rep
+        a, b = g[f].view(np.uint32), ref[f].view(np.uint32)
+        bad = np.count_nonzero(a != b)
+        assert bad == 0, f"{tag}: {f} differs in {bad} of {a.size} segments"
+    num, med, avg = (ref[f].reshape(R, K) for f in ("num", "med", "avg"))
+    gr, gi = O.scores(num, med, avg, hist=hist)
+    er = np.max(np.abs(res.gpu_relative - gr) / np.abs(gr))
+    ei = np.max(np.abs(res.gpu_individual - gi) / np.abs(gi))
+    print(f"\n{tag}: max rel error vs oracle: relative {er:.3e}, individual {ei:.3e} "
+          f"(R={R}, K={K}, stragglers {np.nonzero(res.stragglers_relative)[0][:8].tolist()}...)")
+    np.testing.assert_allclose(res.gpu_relative, gr, rtol=SCORE_RTOL, atol=0)
+    np.testing.assert_allclose(res.gpu_individual, gi, rtol=SCORE_RTOL, atol=0)
+    assert np.array_equal(res.stragglers_relative, O.stragglers(gr, THR).astype(bool)), tag
+    assert np.array_equal(res.stragglers_individual, O.stragglers(gi, THR).astype(bool)), tag
+    assert res.err == 0
+    return gr, gi
 
 
-def test_config1_full_size():
-    R, K, S, cap = 64, 2048, 10000, 8192
-    ns, rep = _check_permutation(R, K, S, cap)
-    # 4 whole rank rows (incl. the straggler rank) against the oracle, bit for bit
-    rows = sorted({0, int(np.nonzero(synth.straggler_ranks(R))[0][0]), 31, 63})
-    host = ns[rows].contiguous().cpu().numpy().view(np.uint32).reshape(-1)
-    st = O.matrix_stats(host, len(rows) * K, S, 0, S, cap, nthreads=16)
-    g = _stats_host(rep)
-    idx = np.concatenate([np.arange(r * K, (r + 1) * K) for r in rows])
-    for f in ("num", "min", "max", "med"):
-        assert np.array_equal(g[f][idx].view(np.uint32), st[f].view(np.uint32)), f
-    _check_mean_std(host.reshape(len(rows) * K, S)[:, S - min(S, cap):], g, idx)
-
-
-def test_config2_full_size():
-    R, K, S, cap = 4096, 2048, 1024, 8192
-    ns, rep = _check_permutation(R, K, S, cap)
-    rows = [0, 1234, 4095]
-    host = ns[rows].contiguous().cpu().numpy().view(np.uint32).reshape(-1)
-    st = O.matrix_stats(host, len(rows) * K, S, 0, S, cap, nthreads=16)
-    g = _stats_host(rep)
-    idx = np.concatenate([np.arange(r * K, (r + 1) * K) for r in rows])
-    for f in ("num", "min", "max", "med"):
-        assert np.array_equal(g[f][idx].view(np.uint32), st[f].view(np.uint32)), f
-    _check_mean_std(host.reshape(len(rows) * K, S), g, idx)
-    del ns, rep
+def _matrix_world(R, K, S, cap, chunk_ranks, permutation=True):
+    seeds = (synth.SEED, synth.SEED ^ 0x1234)
+    rep = batch.MatrixReporter(R, K, cap=cap, thr_rel=THR, thr_ind=THR)
+    hist = np.full((R, K), np.inf)
+    ns = None
+    for i, seed in enumerate(seeds):
+        strag = synth.straggler_ranks(R, seed)
+        ns = synth.synth_matrix(R, K, S, seed=seed, out=ns)
+        res = rep.report(ns, S)
+        g = _stats_host(rep)
+        ref = _matrix_oracle_stats(ns, R, K, S, cap, chunk_ranks)
+        _check_report(f"R={R} K={K} S={S} report {i + 1}", R, K, g, ref, res, hist)
+        assert np.array_equal(res.stragglers_relative, strag.astype(bool))
+        keep = min(S, cap)
+        # FAST AVG / STD: exact mean / population std of the retained samples, rounded once
+        # (DESIGN.md 4); checked on a few whole rank rows
+        rows = sorted({0, int(np.nonzero(strag)[0][0]), R - 1})
+        kept = ns[rows].cpu().numpy().view(np.uint32).reshape(len(rows) * K, S)[:, S - keep:]
+        x = kept.astype(np.float64) / 1000.0
+        idx = np.concatenate([np.arange(r * K, (r + 1) * K) for r in rows])
+        np.testing.assert_allclose(g["avg"][idx], x.mean(axis=1), rtol=2.5e-7, atol=0)
+        np.testing.assert_allclose(g["std"][idx], x.std(axis=1), rtol=1e-6, atol=0)
+    if permutation:
+        # computeStats sorts: reversing every retained window changes nothing
+        flat = ns.view(R * K, S)
+        keep = min(S, cap)
+        flat[:, S - keep:] = torch.flip(flat[:, S - keep:], dims=[1])
+        rep2 = batch.MatrixReporter(R, K, cap=cap, thr_rel=THR, thr_ind=THR)
+        res2 = rep2.report(ns, S)
+        b = _stats_host(rep2)
+        for f in EXACT_FIELDS + ("avg",):
+            assert np.array_equal(g[f].view(np.uint32), b[f].view(np.uint32)), f
+        np.testing.assert_allclose(b["std"], g["std"], rtol=2.5e-7, atol=0)
+        np.testing.assert_allclose(res2.gpu_relative, res.gpu_relative, rtol=1e-12)
+    del ns
     torch.cuda.empty_cache()
 
 
-def test_config3_full_size():
-    # configs[3]: 16,384 Zipf record streams.  A few whole streams against the oracle's
-    # ring-push + computeStats restatement; every stream reversed (push order is free when no
-    # ring overflows: kernel 1 is pushed exactly cap = 8192 times) gives the same statistics
+def test_config0_shape_full_world():
+    # the reference's CPU case shape (BASELINE configs[0]): 8 ranks x 200 kernels x 1000
+    _matrix_world(8, 200, 1000, 8192, chunk_ranks=8)
+
+
+def test_config1_full_world():
+    _matrix_world(64, 2048, 10000, 8192, chunk_ranks=16)
+
+
+def test_config2_full_world():
+    _matrix_world(4096, 2048, 1024, 8192, chunk_ranks=256)
+
+
+def test_config3_full_world():
+    # configs[3]: every one of the 16,384 record streams against the oracle's ring pushes +
+    # computeStats; kernel 1 is pushed exactly cap = 8192 times, so no ring overflows and the
+    # reversed streams must give the same statistics
     R, K, cap = 16384, 2048, 8192
     counts = synth.zipf_counts(K)
     slot, occ = synth.zipf_order(counts)
     N = slot.size
     t = lambda a: torch.from_numpy(a.view(np.int32)).cuda()  # noqa: E731
-    recs = synth.synth_records(R, t(slot), t(occ), K, int(counts.max()))
     rec_off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * N
-    rep = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
-    res = rep.report_records(recs, rec_off)
-    assert np.array_equal(res.stragglers_relative, synth.straggler_ranks(R).astype(bool))
-    a = _stats_host(rep)
-    rows = [0, int(np.nonzero(synth.straggler_ranks(R))[0][0]), R - 1]
-    for r in rows:
-        h = recs[r * N:(r + 1) * N].cpu().numpy().view(np.uint32)
-        ref = O.records_stats(h, np.array([0, N], np.int64), K, cap=cap, nthreads=8)
-        sl = slice(r * K, (r + 1) * K)
-        for f in ("num", "min", "max", "med"):
-            assert np.array_equal(a[f][sl].view(np.uint32), ref[f].view(np.uint32)), (r, f)
+    h_off = np.arange(R + 1, dtype=np.int64) * N
+    rep = batch.MatrixReporter(R, K, cap=cap, thr_rel=THR, thr_ind=THR)
+    hist = np.full((R, K), np.inf)
+    recs = None
+    for i, seed in enumerate((synth.SEED, synth.SEED ^ 0x1234)):
+        strag = synth.straggler_ranks(R, seed)
+        recs = synth.synth_records(R, t(slot), t(occ), K, int(counts.max()), seed=seed, out=recs)
+        res = rep.report_records(recs, rec_off)
+        g = _stats_host(rep)
+        h = recs.cpu().numpy().view(np.uint32)
+        ref = O.records_stats(h, h_off, K, cap=cap, nthreads=THREADS)
+        del h
+        _check_report(f"zipf R={R} report {i + 1}", R, K, g, ref, res, hist)
+        assert np.array_equal(res.stragglers_relative, strag.astype(bool))
         short = ref["num"] <= 128  # lane classes: every field bit-exact
         for f in ("avg", "std"):
-            assert np.array_equal(a[f][sl][short].view(np.uint32), ref[f][short].view(np.uint32)), (r, f)
+            assert np.array_equal(g[f][short].view(np.uint32), ref[f][short].view(np.uint32)), f
     rev = torch.flip(recs.view(R, N, 2), dims=[1]).reshape(R * N, 2)
     del recs
-    rep2 = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    rep2 = batch.MatrixReporter(R, K, cap=cap, thr_rel=THR, thr_ind=THR)
     res2 = rep2.report_records(rev, rec_off)
     b = _stats_host(rep2)
-    for f in ("num", "min", "max", "med"):
-        assert np.array_equal(a[f].view(np.uint32), b[f].view(np.uint32)), f
-    short = a["num"] <= 128
+    for f in EXACT_FIELDS:
+        assert np.array_equal(g[f].view(np.uint32), b[f].view(np.uint32)), f
+    short = g["num"] <= 128
     for f in ("avg", "std"):
-        assert np.array_equal(a[f][short].view(np.uint32), b[f][short].view(np.uint32)), f
-        np.testing.assert_allclose(b[f], a[f], rtol=2.5e-7, atol=0)
+        assert np.array_equal(g[f][short].view(np.uint32), b[f][short].view(np.uint32)), f
+        np.testing.assert_allclose(b[f], g[f], rtol=2.5e-7, atol=0)
     np.testing.assert_allclose(res2.gpu_relative, res.gpu_relative, rtol=1e-12)
     del rev, rep, rep2
     torch.cuda.empty_cache()

@@ -161,3 +161,35 @@ def test_section_summary_matches_torch_semantics(vals):
         assert math.isnan(got[OR.STD])                    # unbiased std of one sample
     else:
         assert got[OR.STD] == pytest.approx(float(torch.std(t)), rel=1e-15)
+
+
+# ---- the oracle's three routes to computeStats give identical statistics: the radix-sorted
+# integer keys (checker), a comparison sort of the converted floats (computeStats' own route),
+# and the std::sort ring-push port that bench.py times as the host-CPU Reporter
+@pytest.mark.parametrize("cap", [8192, 100, 7, 1])
+def test_matrix_stats_routes_agree(cap):
+    rng = np.random.default_rng(cap)
+    parts = [O.gen_matrix(4, 40, 900).reshape(160, 900),
+             rng.integers(0, 2**32, size=(64, 900), dtype=np.uint64).astype(np.uint32),
+             rng.integers(2**24 - 8, 2**24 + 8, size=(32, 900)).astype(np.uint32),  # f32 ties
+             np.full((8, 900), 12345, np.uint32)]
+    ns = np.ascontiguousarray(np.concatenate(parts))
+    r = [O.matrix_stats(ns.reshape(-1), ns.shape[0], 900, 0, 900, cap, nthreads=3, route=x)
+         for x in ("radix", "qsort", "baseline")]
+    for f in r[0]:
+        for other in r[1:]:
+            assert np.array_equal(r[0][f].view(np.uint32), other[f].view(np.uint32)), f
+
+
+@pytest.mark.parametrize("cap", [8192, 5, 1])
+def test_records_stats_routes_agree(cap):
+    rng = np.random.default_rng(11 + cap)
+    R, K, N = 5, 40, 2500
+    slot = rng.integers(0, K + 2, size=R * N).astype(np.uint32)  # a few out-of-range slots
+    ns = rng.integers(1, 2**32, size=R * N, dtype=np.uint64).astype(np.uint32)
+    recs = np.ascontiguousarray(np.stack([slot, ns], 1))
+    off = np.arange(R + 1, dtype=np.int64) * N
+    a = O.records_stats(recs, off, K, cap=cap, nthreads=2)
+    b = O.records_stats(recs, off, K, cap=cap, nthreads=2, route="baseline")
+    for f in a:
+        assert np.array_equal(a[f].view(np.uint32), b[f].view(np.uint32)), f
