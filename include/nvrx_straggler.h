@@ -161,14 +161,16 @@ int nvrx_stragglers(const double* score, int64_t n, double thr, uint8_t* mask, v
 /* Statistics of section CPU timings (ms, float64): section s = vals[off[s] : off[s+1]]
  * (off: [nsec+1], device).  MIN, MAX, MED = lower median s[(n-1)/2] (torch.median),
  * AVG, STD = unbiased (NaN for n == 1), NUM -- Detector._get_section_summaries
- * (straggler.py:171-197).  max_len bounds every section's length (<= 16384). */
+ * (straggler.py:171-197).  max_len bounds every section's length (any length: sections
+ * longer than 16384 timings are sorted in a device scratch buffer instead of LDS). */
 int nvrx_section_stats(const double* vals, const int64_t* off, int64_t nsec, int64_t max_len,
                        int32_t* num, double* mn, double* mx, double* med, double* avg,
                        double* sd, void* stream);
 
 /* ---------------------------------------------------------------- record streams */
 /* A record is one kernel execution: the slot of its composite kernel name and its
- * duration in ns (end - start, CuptiProfiler.cpp:187; clamped to UINT32_MAX). */
+ * duration in ns (end - start, CuptiProfiler.cpp:187; saturated at UINT32_MAX = 4.29 s,
+ * counted by nvrx_profiler_saturated). */
 typedef struct nvrx_record {
     uint32_t slot;
     uint32_t ns;
@@ -221,11 +223,29 @@ int nvrx_profiler_stop(nvrx_profiler* p);
 int nvrx_profiler_reset(nvrx_profiler* p);
 /* Register a composite kernel name ("%s_blk_%d_%d_%d_grid_%d_%d_%d") -> slot. */
 int nvrx_profiler_register_kernel(nvrx_profiler* p, const char* name, uint32_t* slot);
-/* Append host records (push order).  Ignored while stopped (records are dropped). */
+/* Slots are valid until the next nvrx_profiler_reset, which forgets every kernel (the
+ * reference clears its per-kernel map, CuptiProfiler.cpp:148-152): names are registered again
+ * (from slot 0) in the next report interval. */
+/* Append host records (push order).  Ignored while stopped (records are dropped).  Staged
+ * host records move to the device log once buffer_size bytes of them wait (and at every
+ * get_stats / get_records / reset). */
 int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n);
+/* Append n DEVICE records (push order, after every record staged before) to the device log:
+ * one device-to-device copy enqueued on `stream`, so dev_recs must stay valid until that
+ * stream reaches it; later profiler calls order themselves after it.  Ignored while stopped.
+ * Records whose slot is not registered are not counted.  (While a live capture is started,
+ * the copy is itself a kernel dispatch and is recorded like any other.)  No reference
+ * counterpart: the device-side entry of an external tracer (SURVEY 8(b)
+ * nvrx_ingest_records). */
+int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n, void* stream);
+/* Durations longer than UINT32_MAX ns (4.29 s) are stored saturated at UINT32_MAX; *count =
+ * how many since the last reset (the Python layer warns when it is nonzero). */
+int nvrx_profiler_saturated(nvrx_profiler* p, int64_t* count);
 /* Flush, then compute stats of every slot with >= 1 record.  Synchronous.
  * Returns the number of kernels in *count; fills up to `cap_out` entries of slots
- * (sorted by kernel name, as std::map in getStats) and host SoA outputs. */
+ * (sorted by kernel name, as std::map in getStats) and host SoA outputs.  The result is
+ * cached: a size query (cap_out = 0) followed by the copying call computes once, unless
+ * records arrived in between. */
 int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
                             int32_t* num, float* mn, float* mx, float* med, float* avg,
                             float* sd);

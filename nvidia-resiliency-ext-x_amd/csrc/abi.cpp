@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -169,7 +170,6 @@ int nvrx_section_stats(const double* vals, const int64_t* off, int64_t nsec, int
     NVRX_CHECK_ARG(nsec >= 0 && max_len >= 0, "nvrx_section_stats: negative size");
     NVRX_CHECK_ARG(nsec == 0 || (vals && off && num && mn && mx && med && avg && sd),
                    "nvrx_section_stats: null array");
-    NVRX_CHECK_ARG(max_len <= 16384, "nvrx_section_stats: more than 16384 timings per section");
     return hip_status(nvrx::section_stats(vals, off, nsec, max_len, num, mn, mx, med, avg, sd,
                                           S(stream)),
                       "nvrx_section_stats");
@@ -229,16 +229,36 @@ struct nvrx_profiler {
     std::mutex mu;
     bool initialized = false;
     bool started = false;
+    // kernels seen since the last reset (the keys of CuptiProfiler's _kernelDurations map,
+    // which reset() clears, CuptiProfiler.cpp:148-152): slots are renumbered from 0 after
+    // every reset, so a long job with changing launch shapes never runs out of slots
     std::unordered_map<std::string, uint32_t> name_to_slot;
     std::vector<std::string> names;
-    std::vector<nvrx_record> staged;  // host records not yet flushed to the device log
+    // live-capture fast path: (kernel id, block, grid) -> slot, no string work per record
+    std::unordered_map<nvrx::DispatchKey, uint32_t, nvrx::DispatchKeyHash> key_to_slot;
+    std::vector<nvrx_record> staged;  // host records not yet in the device log
+    uint64_t saturated = 0;           // durations clamped to UINT32_MAX ns since the last reset
+    uint64_t version = 0;             // bumped whenever the record set changes
     hipStream_t stream = nullptr;
+    hipEvent_t ingest_ev = nullptr;   // last nvrx_profiler_ingest copy (on the caller's stream)
+    bool ingest_pending = false;
     // device record log (push order since the last reset)
     nvrx_record* d_log = nullptr;
     int64_t log_n = 0, log_cap = 0;
+    nvrx_record* h_pinned = nullptr;  // pinned staging of the host -> device drain
+    int64_t pinned_cap = 0;
     // work buffers (grown on demand)
     void* d_work = nullptr;
     size_t work_bytes = 0;
+    // the last get_stats result (name-sorted), valid while version == cache_version
+    uint64_t cache_version = ~(uint64_t)0;
+    std::vector<uint32_t> c_slot;
+    std::vector<int32_t> c_num;
+    std::vector<float> c_mn, c_mx, c_med, c_avg, c_sd;
+    // staged host records move to the device log once `drain_records` wait (at push, and
+    // at stop for the live capture -- on the caller's thread, never on rocprofiler's), so
+    // host memory stays bounded between reports
+    int64_t drain_records = (int64_t)1 << 16;
 };
 
 namespace {
@@ -343,21 +363,38 @@ int bucket_log(nvrx_profiler* p, int64_t nslots, int force_stable, Work& w) {
     return hip_status(e, "nvrx_profiler: records_bucket");
 }
 
-// Flush staged host records into the device log; compact the log when it is much
-// larger than what the rings can retain.  Caller holds p->mu.
+// Move staged host records into the device log (through a pinned buffer: a DMA copy, no
+// kernel launch that a started capture could record); compact the log when it is much larger
+// than what the rings can retain.  Caller holds p->mu.
 int flush_locked(nvrx_profiler* p) {
     DeviceGuard g(p->cfg.device);
+    if (p->ingest_pending) {  // device-ingested records were copied on the caller's stream
+        hipError_t e = hipStreamWaitEvent(p->stream, p->ingest_ev, 0);
+        if (e != hipSuccess) return hip_status(e, "nvrx_profiler: wait for ingest");
+        p->ingest_pending = false;
+    }
     if (!p->staged.empty()) {
         const int64_t add = (int64_t)p->staged.size();
         int rc = grow_log(p, p->log_n + add);
         if (rc) return rc;
-        hipError_t e = hipMemcpyAsync(p->d_log + p->log_n, p->staged.data(),
+        if (add > p->pinned_cap) {
+            if (p->h_pinned) (void)hipHostFree(p->h_pinned);
+            p->h_pinned = nullptr;
+            p->pinned_cap = 0;
+            const int64_t c = std::max<int64_t>(add, p->drain_records);
+            hipError_t e = hipHostMalloc((void**)&p->h_pinned, (size_t)c * sizeof(nvrx_record), 0);
+            if (e != hipSuccess) return hip_status(e, "nvrx_profiler: hipHostMalloc(staging)");
+            p->pinned_cap = c;
+        }
+        std::memcpy(p->h_pinned, p->staged.data(), (size_t)add * sizeof(nvrx_record));
+        hipError_t e = hipMemcpyAsync(p->d_log + p->log_n, p->h_pinned,
                                       (size_t)add * sizeof(nvrx_record), hipMemcpyHostToDevice,
                                       p->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
         if (e != hipSuccess) return hip_status(e, "nvrx_profiler: flush");
         p->log_n += add;
         p->staged.clear();
+        if (p->staged.capacity() > (size_t)4 * p->drain_records) p->staged.shrink_to_fit();
     }
     const int64_t nslots = (int64_t)p->names.size();
     const int64_t cap = p->cfg.stats_max_len_per_kernel;
@@ -396,27 +433,46 @@ int flush_locked(nvrx_profiler* p) {
     return NVRX_OK;
 }
 
+uint32_t slot_of_name(nvrx_profiler* p, const std::string& key) {
+    auto it = p->name_to_slot.find(key);
+    if (it != p->name_to_slot.end()) return it->second;
+    const uint32_t slot = (uint32_t)p->names.size();
+    p->name_to_slot.emplace(key, slot);
+    p->names.push_back(key);
+    return slot;
+}
+
 }  // namespace
 
 namespace nvrx {
-// capture.cpp's dispatch callback: one completed kernel under its composite key
-// The dispatch context only produces records for kernels enqueued while it was started;
-// such a kernel may complete (and its record arrive) after stop, and is still counted, as
-// CUPTI delivers the activity records of kernels launched while the activity kind was
-// enabled (bufferCompleted, CuptiProfiler.cpp:168-203, pushes regardless of _isStarted).
-void profiler_push_named(nvrx_profiler* p, const char* key, uint32_t ns) {
-    std::lock_guard<std::mutex> lk(p->mu);
-    if (!p->initialized) return;
-    auto it = p->name_to_slot.find(key);
-    uint32_t slot;
-    if (it != p->name_to_slot.end()) {
-        slot = it->second;
-    } else {
-        slot = (uint32_t)p->names.size();
-        p->name_to_slot.emplace(key, slot);
-        p->names.emplace_back(key);
+// capture.cpp's buffer callback: one delivered batch of completed dispatches.  A dispatch
+// enqueued while the profiler was started may complete (and its record arrive) after stop;
+// it is still counted, as CUPTI delivers the activity records of kernels launched while the
+// activity kind was enabled (bufferCompleted, CuptiProfiler.cpp:168-203, pushes regardless
+// of _isStarted).
+void profiler_push_dispatches(nvrx_profiler* p, const DispatchRec* r, size_t n,
+                              std::string (*composite_name)(const DispatchKey&)) {
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        if (!p->initialized) return;
+        for (size_t i = 0; i < n; ++i) {
+            uint32_t slot;
+            auto it = p->key_to_slot.find(r[i].key);
+            if (it != p->key_to_slot.end()) {
+                slot = it->second;
+            } else {
+                slot = slot_of_name(p, composite_name(r[i].key));  // CuptiProfiler.cpp:182-185
+                p->key_to_slot.emplace(r[i].key, slot);
+            }
+            uint32_t ns = (uint32_t)r[i].ns;
+            if (r[i].ns > 0xFFFFFFFFull) {  // > 4.29 s: saturate, counted
+                ns = 0xFFFFFFFFu;
+                ++p->saturated;
+            }
+            p->staged.push_back(nvrx_record{slot, ns});
+        }
+        ++p->version;
     }
-    p->staged.push_back(nvrx_record{slot, ns});
 }
 }  // namespace nvrx
 
@@ -434,12 +490,17 @@ int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
         return fail(NVRX_ERR_SINGLETON, "Only one CuptiProfiler instance is allowed.");
     auto* p = new nvrx_profiler();
     p->cfg = *cfg;
+    // the drain watermark follows the host buffer size (CUPTI bufferSize, cupti.py:25)
+    if (cfg->buffer_size >= (int64_t)sizeof(nvrx_record) * 1024)
+        p->drain_records = cfg->buffer_size / (int64_t)sizeof(nvrx_record);
     {
         DeviceGuard g(cfg->device);
         hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ingest_ev, hipEventDisableTiming);
         if (e != hipSuccess) {
+            if (p->stream) (void)hipStreamDestroy(p->stream);
             delete p;
-            return hip_status(e, "nvrx_profiler_create: hipStreamCreate");
+            return hip_status(e, "nvrx_profiler_create: stream/event");
         }
     }
     g_instance = p;
@@ -449,6 +510,8 @@ int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
 
 int nvrx_profiler_destroy(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_destroy: null handle");
+    // no capture callback may touch the handle after this: capture_detach delivers what is
+    // pending, unhooks the handle and waits for any callback still running
     nvrx::capture_detach(p);
     {
         std::lock_guard<std::mutex> lk(g_instance_mu);
@@ -456,8 +519,11 @@ int nvrx_profiler_destroy(nvrx_profiler* p) {
     }
     {
         DeviceGuard g(p->cfg.device);
+        if (p->stream) (void)hipStreamSynchronize(p->stream);
         if (p->d_log) (void)hipFree(p->d_log);
         if (p->d_work) (void)hipFree(p->d_work);
+        if (p->h_pinned) (void)hipHostFree(p->h_pinned);
+        if (p->ingest_ev) (void)hipEventDestroy(p->ingest_ev);
         if (p->stream) (void)hipStreamDestroy(p->stream);
     }
     delete p;
@@ -498,13 +564,14 @@ int nvrx_profiler_start(nvrx_profiler* p) {
 
 int nvrx_profiler_stop(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_stop: null handle");
-    // deliver the dispatches that completed while started, outside the handle lock (the
-    // buffer callback takes it)
     const int rc = nvrx::capture_stop(p);
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->started) std::fprintf(stderr, "CuptiProfiler::stopProfiling called while not profiling.\n");
     p->started = false;
     if (rc != 0) return fail(NVRX_ERR_STATE, "nvrx_profiler_stop: rocprofiler_stop_context failed");
+    // bounded host memory: what the capture delivered so far moves to the device log here,
+    // on the caller's thread, once a buffer's worth waits
+    if ((int64_t)p->staged.size() >= p->drain_records) return flush_locked(p);
     return NVRX_OK;
 }
 
@@ -512,23 +579,27 @@ int nvrx_profiler_reset(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_reset: null handle");
     (void)nvrx::capture_flush();  // CuptiProfiler.cpp:149: flush, then clear (outside the lock)
     std::lock_guard<std::mutex> lk(p->mu);
-    p->staged.clear();  // CuptiProfiler.cpp:148-152: flush + clear all rings
+    DeviceGuard g(p->cfg.device);
+    if (p->ingest_pending) {  // an ingest copy may still target the log
+        (void)hipEventSynchronize(p->ingest_ev);
+        p->ingest_pending = false;
+    }
+    // CuptiProfiler.cpp:148-152: clear every kernel's ring -- and forget the kernels, so
+    // the slots are renumbered from 0 in the next interval
+    p->staged.clear();
     p->log_n = 0;
+    p->names.clear();
+    p->name_to_slot.clear();
+    p->key_to_slot.clear();
+    p->saturated = 0;
+    ++p->version;
     return NVRX_OK;
 }
 
 int nvrx_profiler_register_kernel(nvrx_profiler* p, const char* name, uint32_t* slot) {
     NVRX_CHECK_ARG(p && name && slot, "nvrx_profiler_register_kernel: null argument");
     std::lock_guard<std::mutex> lk(p->mu);
-    auto it = p->name_to_slot.find(name);
-    if (it != p->name_to_slot.end()) {
-        *slot = it->second;
-        return NVRX_OK;
-    }
-    const uint32_t s = (uint32_t)p->names.size();
-    p->name_to_slot.emplace(name, s);
-    p->names.emplace_back(name);
-    *slot = s;
+    *slot = slot_of_name(p, name);
     return NVRX_OK;
 }
 
@@ -540,63 +611,105 @@ int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n) {
     for (int64_t i = 0; i < n; ++i)
         if (recs[i].slot >= nslots) return fail(NVRX_ERR_INVALID, "nvrx_profiler_push: unknown slot");
     p->staged.insert(p->staged.end(), recs, recs + n);
+    ++p->version;
+    if ((int64_t)p->staged.size() >= p->drain_records) return flush_locked(p);
+    return NVRX_OK;
+}
+
+int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n, void* stream) {
+    NVRX_CHECK_ARG(p && n >= 0 && (n == 0 || dev_recs), "nvrx_profiler_ingest: bad arguments");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->started || n == 0) return NVRX_OK;  // activity disabled: records are not captured
+    DeviceGuard g(p->cfg.device);
+    int rc = flush_locked(p);  // host records staged earlier come first (push order)
+    if (rc) return rc;
+    rc = grow_log(p, p->log_n + n);
+    if (rc) return rc;
+    hipError_t e = hipMemcpyAsync(p->d_log + p->log_n, dev_recs, (size_t)n * sizeof(nvrx_record),
+                                  hipMemcpyDeviceToDevice, S(stream));
+    if (e == hipSuccess) e = hipEventRecord(p->ingest_ev, S(stream));
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler_ingest");
+    p->ingest_pending = true;
+    p->log_n += n;
+    ++p->version;
+    return NVRX_OK;
+}
+
+int nvrx_profiler_saturated(nvrx_profiler* p, int64_t* count) {
+    NVRX_CHECK_ARG(p && count, "nvrx_profiler_saturated: null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    *count = (int64_t)p->saturated;
     return NVRX_OK;
 }
 
 int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
                             int32_t* num, float* mn, float* mx, float* med, float* avg, float* sd) {
-    NVRX_CHECK_ARG(p && count, "nvrx_profiler_get_stats: null argument");
+    NVRX_CHECK_ARG(p && count && cap_out >= 0, "nvrx_profiler_get_stats: bad arguments");
     (void)nvrx::capture_flush();  // CuptiProfiler.cpp:138 cuptiActivityFlushAll (before the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);
     int rc = flush_locked(p);
     if (rc) return rc;
-    *count = 0;
-    const int64_t nslots = (int64_t)p->names.size();
-    const size_t nb = (size_t)nslots * 4;
-    if (p->log_n == 0 || nslots == 0) return NVRX_OK;
-    if (nslots > nvrx_records_max_slots())
-        return fail(NVRX_ERR_INVALID, "nvrx_profiler_get_stats: too many distinct kernels");
-    Work w;
-    rc = bucket_log(p, nslots, 0, w);
-    if (rc) return rc;
-    nvrx_stats_soa soa{w.num, w.mn, w.mx, w.med, w.avg, w.sd};
-    const int64_t cap = p->cfg.stats_max_len_per_kernel;
-    hipError_t e = nvrx::segment_stats_ragged(w.ns, w.seg_off, w.seg_len, nslots,
-                                              std::min<int64_t>(cap, p->log_n), cap, p->cfg.mode,
-                                              true, soa, nullptr, 0, p->stream);
-    if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: segment_stats");
-    std::vector<int32_t> hnum(nslots);
-    std::vector<float> hmn(nslots), hmx(nslots), hmed(nslots), havg(nslots), hsd(nslots);
-    struct {
-        void* dst;
-        const void* src;
-        size_t b;
-    } cps[] = {{hnum.data(), w.num, nb}, {hmn.data(), w.mn, nb},   {hmx.data(), w.mx, nb},
-               {hmed.data(), w.med, nb}, {havg.data(), w.avg, nb}, {hsd.data(), w.sd, nb}};
-    for (auto& c : cps) {
-        e = hipMemcpyAsync(c.dst, c.src, c.b, hipMemcpyDeviceToHost, p->stream);
-        if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: download");
+    if (p->cache_version != p->version) {
+        // recompute (a size query followed by the copy call reuses this result)
+        for (auto* v : {&p->c_mn, &p->c_mx, &p->c_med, &p->c_avg, &p->c_sd}) v->clear();
+        p->c_slot.clear();
+        p->c_num.clear();
+        const int64_t nslots = (int64_t)p->names.size();
+        if (p->log_n > 0 && nslots > 0) {
+            if (nslots > nvrx_records_max_slots())
+                return fail(NVRX_ERR_INVALID,
+                            "nvrx_profiler_get_stats: more distinct kernels in one report interval "
+                            "than nvrx_records_max_slots()");
+            Work w;
+            rc = bucket_log(p, nslots, 0, w);
+            if (rc) return rc;
+            nvrx_stats_soa soa{w.num, w.mn, w.mx, w.med, w.avg, w.sd};
+            const int64_t cap = p->cfg.stats_max_len_per_kernel;
+            hipError_t e = nvrx::segment_stats_ragged(w.ns, w.seg_off, w.seg_len, nslots,
+                                                      std::min<int64_t>(cap, p->log_n), cap,
+                                                      p->cfg.mode, true, soa, nullptr, 0, p->stream);
+            if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: segment_stats");
+            const size_t nb = (size_t)nslots * 4;
+            std::vector<int32_t> hnum(nslots);
+            std::vector<float> hmn(nslots), hmx(nslots), hmed(nslots), havg(nslots), hsd(nslots);
+            struct {
+                void* dst;
+                const void* src;
+            } cps[] = {{hnum.data(), w.num}, {hmn.data(), w.mn},   {hmx.data(), w.mx},
+                       {hmed.data(), w.med}, {havg.data(), w.avg}, {hsd.data(), w.sd}};
+            for (auto& c : cps) {
+                e = hipMemcpyAsync(c.dst, c.src, nb, hipMemcpyDeviceToHost, p->stream);
+                if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: download");
+            }
+            e = hipStreamSynchronize(p->stream);
+            if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: sync");
+            // std::map order of getStats (CuptiProfiler.cpp:137-145): sorted by composite name
+            for (int64_t s = 0; s < nslots; ++s)
+                if (hnum[s] > 0) p->c_slot.push_back((uint32_t)s);
+            std::sort(p->c_slot.begin(), p->c_slot.end(),
+                      [&](uint32_t a, uint32_t b) { return p->names[a] < p->names[b]; });
+            for (uint32_t s : p->c_slot) {
+                p->c_num.push_back(hnum[s]);
+                p->c_mn.push_back(hmn[s]);
+                p->c_mx.push_back(hmx[s]);
+                p->c_med.push_back(hmed[s]);
+                p->c_avg.push_back(havg[s]);
+                p->c_sd.push_back(hsd[s]);
+            }
+        }
+        p->cache_version = p->version;
     }
-    e = hipStreamSynchronize(p->stream);
-    if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: sync");
-    // std::map order of getStats (CuptiProfiler.cpp:137-145): sorted by composite name
-    std::vector<uint32_t> order;
-    for (int64_t s = 0; s < nslots; ++s)
-        if (hnum[s] > 0) order.push_back((uint32_t)s);
-    std::sort(order.begin(), order.end(),
-              [&](uint32_t a, uint32_t b) { return p->names[a] < p->names[b]; });
-    *count = (int64_t)order.size();
-    const int64_t m = std::min<int64_t>(cap_out, (int64_t)order.size());
+    *count = (int64_t)p->c_slot.size();
+    const int64_t m = std::min<int64_t>(cap_out, *count);
     for (int64_t i = 0; i < m; ++i) {
-        const uint32_t s = order[i];
-        if (slots) slots[i] = s;
-        if (num) num[i] = hnum[s];
-        if (mn) mn[i] = hmn[s];
-        if (mx) mx[i] = hmx[s];
-        if (med) med[i] = hmed[s];
-        if (avg) avg[i] = havg[s];
-        if (sd) sd[i] = hsd[s];
+        if (slots) slots[i] = p->c_slot[i];
+        if (num) num[i] = p->c_num[i];
+        if (mn) mn[i] = p->c_mn[i];
+        if (mx) mx[i] = p->c_mx[i];
+        if (med) med[i] = p->c_med[i];
+        if (avg) avg[i] = p->c_avg[i];
+        if (sd) sd[i] = p->c_sd[i];
     }
     return NVRX_OK;
 }

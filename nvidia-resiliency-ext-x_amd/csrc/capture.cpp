@@ -19,13 +19,16 @@
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
+#include <vector>
 
 #include "nvrx_internal.h"
 
@@ -40,6 +43,9 @@ struct Capture {
     std::atomic<bool> ready{false};      // tool_init completed
     std::atomic<bool> requested{false};  // nvrx_capture_configure succeeded
     std::atomic<nvrx_profiler*> target{nullptr};
+    std::atomic<int> inflight{0};        // buffer callbacks running (destroy waits for 0)
+    std::atomic<uint64_t> n_cb{0}, n_rec{0}, n_pushed{0};  // NVRX_CAPTURE_DEBUG=1 counters
+    bool debug = false;
     // diagnostics of the capture's cost (tools/live_gpt2.py):
     bool discard = false;       // NVRX_CAPTURE_DISCARD=1: drop records (the tracer alone)
     bool keep_started = false;  // NVRX_CAPTURE_KEEP_STARTED=1: never stop the dispatch context
@@ -65,42 +71,61 @@ void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_us
     cap().names[d->kernel_id] = std::move(n);
 }
 
+// CuptiProfiler.cpp:182-185: "%s_blk_%d_%d_%d_grid_%d_%d_%d" (only for a key the profiler
+// has not seen since its last reset; known keys map to their slot without string work)
+std::string composite_name(const nvrx::DispatchKey& k) {
+    std::string name;
+    {
+        std::lock_guard<std::mutex> lk(cap().mu);
+        auto it = cap().names.find(k.kernel_id);
+        name = it != cap().names.end() ? it->second : std::string("unknown_kernel");
+    }
+    std::vector<char> buf(name.size() + 96);
+    std::snprintf(buf.data(), buf.size(), "%s_blk_%d_%d_%d_grid_%d_%d_%d", name.c_str(), (int)k.bx,
+                  (int)k.by, (int)k.bz, (int)k.gx, (int)k.gy, (int)k.gz);
+    return std::string(buf.data());
+}
+
 void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
                         rocprofiler_record_header_t** headers, size_t num_headers, void*,
                         uint64_t) {
-    nvrx_profiler* p = cap().target.load();
-    if (!p || cap().discard) return;
-    char key[4096];
-    for (size_t i = 0; i < num_headers; ++i) {
-        const rocprofiler_record_header_t* h = headers[i];
-        if (h->category != ROCPROFILER_BUFFER_CATEGORY_TRACING ||
-            h->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
-            continue;
-        auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
-        const rocprofiler_kernel_dispatch_info_t& di = r->dispatch_info;
-        std::string name;
-        {
-            std::lock_guard<std::mutex> lk(cap().mu);
-            auto it = cap().names.find(di.kernel_id);
-            name = it != cap().names.end() ? it->second : std::string("unknown_kernel");
+    Capture& c = cap();
+    // in-flight count first, then the target: capture_detach clears the target and then
+    // waits for the count to drain, so a callback never touches a destroyed handle
+    c.inflight.fetch_add(1);
+    nvrx_profiler* p = c.target.load();
+    if (p && !c.discard) {
+        thread_local std::vector<nvrx::DispatchRec> batch;
+        batch.clear();
+        for (size_t i = 0; i < num_headers; ++i) {
+            const rocprofiler_record_header_t* h = headers[i];
+            if (h->category != ROCPROFILER_BUFFER_CATEGORY_TRACING ||
+                h->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
+                continue;
+            auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
+            const rocprofiler_kernel_dispatch_info_t& di = r->dispatch_info;
+            // block dims = workgroup size; grid_size is in work-items, CUPTI's grid in blocks
+            const uint32_t bx = di.workgroup_size.x, by = di.workgroup_size.y, bz = di.workgroup_size.z;
+            nvrx::DispatchRec d;
+            d.key = {di.kernel_id, bx, by, bz, bx ? di.grid_size.x / bx : 0,
+                     by ? di.grid_size.y / by : 0, bz ? di.grid_size.z / bz : 0};
+            d.ns = r->end_timestamp > r->start_timestamp ? r->end_timestamp - r->start_timestamp : 0;
+            batch.push_back(d);
         }
-        const uint32_t bx = di.workgroup_size.x, by = di.workgroup_size.y, bz = di.workgroup_size.z;
-        const uint32_t gx = bx ? di.grid_size.x / bx : 0, gy = by ? di.grid_size.y / by : 0,
-                       gz = bz ? di.grid_size.z / bz : 0;
-        // CuptiProfiler.cpp:182-185
-        std::snprintf(key, sizeof(key), "%s_blk_%d_%d_%d_grid_%d_%d_%d", name.c_str(), (int)bx,
-                      (int)by, (int)bz, (int)gx, (int)gy, (int)gz);
-        const uint64_t dt = r->end_timestamp > r->start_timestamp
-                                ? r->end_timestamp - r->start_timestamp
-                                : 0;
-        nvrx::profiler_push_named(p, key, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt);
+        c.n_cb.fetch_add(1);
+        c.n_rec.fetch_add(num_headers);
+        c.n_pushed.fetch_add(batch.size());
+        if (!batch.empty()) nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
     }
+    c.inflight.fetch_sub(1);
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
     Capture& c = cap();
     const char* d = std::getenv("NVRX_CAPTURE_DISCARD");
     c.discard = d && d[0] == '1';
+    const char* dbg = std::getenv("NVRX_CAPTURE_DEBUG");
+    c.debug = dbg && dbg[0] == '1';
     const char* k = std::getenv("NVRX_CAPTURE_KEEP_STARTED");
     c.keep_started = k && k[0] == '1';
     if (rocprofiler_create_context(&c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
@@ -111,7 +136,10 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
         return -1;
     if (rocprofiler_create_context(&c.disp_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
     size_t watermark = 1u << 20;  // ~ the Detector's CUPTI bufferSize (1 MB, cupti.py:25)
-    if (const char* w = std::getenv("NVRX_CAPTURE_WATERMARK")) watermark = std::strtoull(w, nullptr, 10);
+    // NVRX_CAPTURE_WATERMARK overrides it, not below 64 KiB: with watermarks of a few KB
+    // rocprofiler-sdk (ROCm 7.2) was measured to lose dispatch records (tools/diag_capture.py)
+    if (const char* w = std::getenv("NVRX_CAPTURE_WATERMARK"))
+        watermark = std::max<size_t>(std::strtoull(w, nullptr, 10), (size_t)64 << 10);
     if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, watermark, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
                                   dispatch_buffer_cb, nullptr, &c.buffer) != ROCPROFILER_STATUS_SUCCESS)
         return -1;
@@ -170,9 +198,16 @@ int capture_flush() {
 
 void capture_detach(nvrx_profiler* p) {
     Capture& c = cap();
+    if (c.target.load() != p) return;
+    if (c.ready) (void)rocprofiler_flush_buffer(c.buffer);  // deliver what is pending, to p
     nvrx_profiler* cur = p;
     if (c.target.compare_exchange_strong(cur, nullptr) && c.ready)
         (void)rocprofiler_stop_context(c.disp_ctx);
+    while (c.inflight.load() != 0) std::this_thread::yield();  // callbacks that loaded p
+    if (c.debug)
+        std::fprintf(stderr, "nvrx capture: %llu callbacks, %llu headers, %llu dispatch records\n",
+                     (unsigned long long)c.n_cb.load(), (unsigned long long)c.n_rec.load(),
+                     (unsigned long long)c.n_pushed.load());
 }
 
 }  // namespace nvrx

@@ -48,7 +48,31 @@ hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, cons
 // abi.cpp <-> capture.cpp
 #include <string>
 void set_error(const std::string& msg);
-void profiler_push_named(nvrx_profiler* p, const char* key, uint32_t ns);
+// one completed dispatch: what the reference's composite key is built from
+// (CuptiProfiler.cpp:182-185: kernel name, block dims, grid dims in blocks)
+struct DispatchKey {
+    uint64_t kernel_id;
+    uint32_t bx, by, bz, gx, gy, gz;
+    bool operator==(const DispatchKey& o) const {
+        return kernel_id == o.kernel_id && bx == o.bx && by == o.by && bz == o.bz && gx == o.gx &&
+               gy == o.gy && gz == o.gz;
+    }
+};
+struct DispatchKeyHash {
+    size_t operator()(const DispatchKey& k) const {
+        uint64_t h = k.kernel_id * 0x9E3779B97F4A7C15ull;
+        for (uint32_t v : {k.bx, k.by, k.bz, k.gx, k.gy, k.gz}) h = (h ^ v) * 0x100000001B3ull;
+        return (size_t)(h ^ (h >> 29));
+    }
+};
+struct DispatchRec {
+    DispatchKey key;
+    uint64_t ns;  // end - start
+};
+// push one delivered batch; composite_name builds "%s_blk_%d_%d_%d_grid_%d_%d_%d" for a key
+// the profiler has not seen since its last reset
+void profiler_push_dispatches(nvrx_profiler* p, const DispatchRec* r, size_t n,
+                              std::string (*composite_name)(const DispatchKey&));
 bool capture_ready();
 int capture_start(nvrx_profiler* p);
 int capture_stop(nvrx_profiler* p);

@@ -7,20 +7,21 @@
 // One 256-thread workgroup per section: values staged in LDS, bitonic sort (+inf
 // padding), then order statistics; mean / variance by a fixed-order tree over the
 // sorted values (float64; torch's own summation order is not specified, so AVG/STD
-// match to ~1e-16 relative, MIN/MAX/MED exactly).
+// match to ~1e-16 relative, MIN/MAX/MED exactly).  Sections longer than 16384 timings
+// (CustomSection.max_elapseds_len raised by the user) are sorted the same way in a device
+// scratch buffer by a 1024-thread workgroup.
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
 namespace nvrx {
 
-template <int NMAX>
-__global__ __launch_bounds__(256) void section_stats_kernel(const double* __restrict__ vals,
-                                                            const int64_t* __restrict__ off,
-                                                            int32_t* num, double* mn, double* mx,
-                                                            double* med, double* avg, double* sd) {
-    __shared__ double s[NMAX];
-    __shared__ double red[256];
-    const int64_t sec = blockIdx.x;
+// The statistics of one section, every thread of the block: s (LDS, or this block's
+// device scratch) gets the values padded with +inf to a power of two and sorted.
+template <int NT>
+__device__ __forceinline__ void section_body(const double* __restrict__ vals, const int64_t* off,
+                                             int64_t sec, double* s, double* red, int32_t* num,
+                                             double* mn, double* mx, double* med, double* avg,
+                                             double* sd) {
     const int64_t b = off[sec];
     const int n = (int)(off[sec + 1] - b);
     const int tid = threadIdx.x;
@@ -34,11 +35,11 @@ __global__ __launch_bounds__(256) void section_stats_kernel(const double* __rest
     }
     int np2 = 1;
     while (np2 < n) np2 <<= 1;
-    for (int i = tid; i < np2; i += 256) s[i] = i < n ? vals[b + i] : __builtin_inf();
+    for (int i = tid; i < np2; i += NT) s[i] = i < n ? vals[b + i] : __builtin_inf();
     __syncthreads();
     for (int k = 2; k <= np2; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < np2; i += 256) {
+            for (int i = tid; i < np2; i += NT) {
                 const int ixj = i ^ j;
                 if (ixj > i) {
                     const double x = s[i], y = s[ixj];
@@ -54,23 +55,23 @@ __global__ __launch_bounds__(256) void section_stats_kernel(const double* __rest
     }
     // mean: per-thread strided partial sums, then a fixed tree
     double acc = 0.0;
-    for (int i = tid; i < n; i += 256) acc += s[i];
+    for (int i = tid; i < n; i += NT) acc += s[i];
     red[tid] = acc;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = NT / 2; w > 0; w >>= 1) {
         if (tid < w) red[tid] = red[tid] + red[tid + w];
         __syncthreads();
     }
     const double mean = red[0] / (double)n;
     __syncthreads();
     double q = 0.0;
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += NT) {
         const double d = s[i] - mean;
         q += d * d;
     }
     red[tid] = q;
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = NT / 2; w > 0; w >>= 1) {
         if (tid < w) red[tid] = red[tid] + red[tid + w];
         __syncthreads();
     }
@@ -82,6 +83,26 @@ __global__ __launch_bounds__(256) void section_stats_kernel(const double* __rest
         avg[sec] = mean;
         sd[sec] = n > 1 ? __builtin_sqrt(red[0] / (double)(n - 1)) : __builtin_nan("");
     }
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void section_stats_kernel(const double* __restrict__ vals,
+                                                            const int64_t* __restrict__ off,
+                                                            int32_t* num, double* mn, double* mx,
+                                                            double* med, double* avg, double* sd) {
+    __shared__ double s[NMAX];
+    __shared__ double red[256];
+    section_body<256>(vals, off, blockIdx.x, s, red, num, mn, mx, med, avg, sd);
+}
+
+// sections longer than the LDS holds: the block's own slice of a device scratch buffer
+// (np2 doubles per section); global stores are visible to the block after __syncthreads
+__global__ __launch_bounds__(1024) void section_stats_global_kernel(
+    const double* __restrict__ vals, const int64_t* __restrict__ off, double* work, int64_t np2,
+    int32_t* num, double* mn, double* mx, double* med, double* avg, double* sd) {
+    __shared__ double red[1024];
+    section_body<1024>(vals, off, blockIdx.x, work + (int64_t)blockIdx.x * np2, red, num, mn, mx,
+                       med, avg, sd);
 }
 
 hipError_t section_stats(const double* vals, const int64_t* off, int64_t nsec, int64_t max_len,
@@ -97,8 +118,18 @@ hipError_t section_stats(const double* vals, const int64_t* off, int64_t nsec, i
     else if (max_len <= 16384)
         hipLaunchKernelGGL(section_stats_kernel<16384>, dim3((unsigned)nsec), dim3(256), 0, st, vals,
                            off, num, mn, mx, med, avg, sd);
-    else
-        return hipErrorInvalidValue;
+    else {
+        if (max_len > ((int64_t)1 << 30)) return hipErrorInvalidValue;
+        int64_t np2 = 1;
+        while (np2 < max_len) np2 <<= 1;
+        void* work = nullptr;
+        hipError_t e = hipMallocAsync(&work, (size_t)(nsec * np2) * sizeof(double), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(section_stats_global_kernel, dim3((unsigned)nsec), dim3(1024), 0, st, vals,
+                           off, (double*)work, np2, num, mn, mx, med, avg, sd);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return hipFreeAsync(work, st);
+    }
     return hipGetLastError();
 }
 

@@ -93,6 +93,8 @@ SIGNATURES = {
     "nvrx_profiler_reset": (ctypes.c_int, [P]),
     "nvrx_profiler_register_kernel": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.POINTER(u32)]),
     "nvrx_profiler_push": (ctypes.c_int, [P, P, i64]),
+    "nvrx_profiler_ingest": (ctypes.c_int, [P, P, i64, P]),
+    "nvrx_profiler_saturated": (ctypes.c_int, [P, ctypes.POINTER(i64)]),
     "nvrx_profiler_get_stats": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P, P, P, P, P, P, P]),
     "nvrx_profiler_kernel_name": (ctypes.c_int, [P, u32, ctypes.c_char_p, i64]),
     "nvrx_profiler_get_records": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P]),

@@ -43,6 +43,30 @@ class KernelStats:
 
 
 _capture_state: Optional[bool] = None
+_tool_env: list = []  # environment variables rocprofiler-sdk's configuration added
+
+
+def _c_environ() -> Dict[str, str]:
+    """The process environment as the C library sees it (os.environ is a start-up snapshot)."""
+    libc = ctypes.CDLL(None)
+    env = ctypes.POINTER(ctypes.c_char_p).in_dll(libc, "environ")
+    out, i = {}, 0
+    while env[i]:
+        k, _, v = env[i].decode(errors="replace").partition("=")
+        out[k] = v
+        i += 1
+    return out
+
+
+def _scrub_tool_env() -> None:
+    """rocprofiler_force_configure exports ROCPROFILER_REGISTER_FORCE_LOAD=1 (and GLOG_*)
+    into this process's environment; inherited by a child process (torchrun workers, test
+    subprocesses) it keeps that child from configuring its own capture.  Once this process's
+    runtime has initialised -- or configuration was refused -- they are removed again."""
+    while _tool_env:
+        k = _tool_env.pop()
+        os.environ.pop(k, None)
+        os.unsetenv(k)
 
 
 def enable_capture() -> bool:
@@ -54,7 +78,11 @@ def enable_capture() -> bool:
         if os.environ.get("NVRX_CAPTURE", "1") == "0":
             _capture_state = False
         else:
+            before = _c_environ()
             _capture_state = N.lib().nvrx_capture_configure() == 0
+            _tool_env.extend(k for k in _c_environ() if k not in before)
+            if not _capture_state:
+                _scrub_tool_env()
     return _capture_state
 
 
@@ -85,6 +113,7 @@ class KernelProfiler:
         N.check(N.lib().nvrx_profiler_create(ctypes.byref(cfg), ctypes.byref(h)),
                 "CuptiProfiler")
         self._h = h
+        _scrub_tool_env()  # the runtime (and the tool, if configured) is initialised now
         self._slot_of: Dict[str, int] = {}
         self._names: list = []
 
@@ -113,7 +142,12 @@ class KernelProfiler:
         N.call("nvrx_profiler_stop", self._h)
 
     def reset(self):
+        """Flush, then clear every kernel's records AND forget the kernels (as the
+        reference's reset clears its per-kernel map, CuptiProfiler.cpp:148-152): slots are
+        renumbered from 0 in the next interval, so the name caches here are dropped too."""
         N.call("nvrx_profiler_reset", self._h)
+        self._slot_of.clear()
+        self._names.clear()
 
     def register_kernel(self, name: str) -> int:
         s = self._slot_of.get(name)
@@ -134,24 +168,59 @@ class KernelProfiler:
         self.push_slots(np.full(d.size, self.register_kernel(name), np.uint32), d)
 
     def push_slots(self, slots: np.ndarray, durations_ns: np.ndarray) -> None:
+        """Records of registered slots (valid until the next reset).  Durations above
+        UINT32_MAX ns (4.29 s) are stored saturated, with a warning (the record format keeps
+        integer ns in 32 bits)."""
+        d = np.asarray(durations_ns, dtype=np.uint64)
+        if d.size and int(d.max()) > 0xFFFFFFFF:
+            warnings.warn(f"{int((d > 0xFFFFFFFF).sum())} kernel duration(s) above 4.29 s stored "
+                          "saturated at 4294967295 ns", RuntimeWarning, stacklevel=2)
         recs = np.empty((len(slots), 2), dtype=np.uint32)
         recs[:, 0] = slots
-        recs[:, 1] = np.minimum(np.asarray(durations_ns, dtype=np.uint64), 0xFFFFFFFF)
+        recs[:, 1] = np.minimum(d, 0xFFFFFFFF)
         N.call("nvrx_profiler_push", self._h, recs.ctypes.data, len(slots))
 
+    def ingest(self, records, stream=None) -> None:
+        """Append DEVICE records: an int32/uint32 tensor [n, 2] of {slot, ns} (registered slots,
+        push order) resident on the profiler's device, copied into the device record log on
+        `stream` (default: the current stream) -- no host round trip."""
+        import torch
+
+        N.require_device(records, "records")
+        if records.dim() != 2 or records.shape[1] != 2 or records.element_size() != 4:
+            raise ValueError("records must be a [n, 2] tensor of 32-bit {slot, ns}")
+        records = records.contiguous()
+        N.call("nvrx_profiler_ingest", self._h, records.data_ptr(), records.shape[0],
+               N.stream_handle(stream if stream is not None else torch.cuda.current_stream(records.device)))
+
+    def saturated(self) -> int:
+        """Durations stored saturated at UINT32_MAX ns since the last reset."""
+        c = ctypes.c_int64()
+        N.call("nvrx_profiler_saturated", self._h, ctypes.byref(c))
+        return int(c.value)
+
     def get_stats_columns(self) -> KernelSummaries:
-        """Per-kernel statistics (HIP) as columns, sorted by composite kernel name."""
+        """Per-kernel statistics (HIP) as columns, sorted by composite kernel name.  One
+        device computation: the size query's result is cached by the library and the copying
+        call reuses it (recomputed only if records arrived in between, hence the loop)."""
         L = N.lib()
         count = ctypes.c_int64()
         N.call("nvrx_profiler_get_stats", self._h, 0, ctypes.byref(count), None, None, None,
                None, None, None, None)
-        n = int(count.value)
-        slots = np.empty(n, np.uint32)
-        num = np.empty(n, np.int32)
-        cols = [np.empty(n, np.float32) for _ in range(5)]
         p = lambda a: a.ctypes.data  # noqa: E731
-        N.check(L.nvrx_profiler_get_stats(self._h, n, ctypes.byref(count), p(slots), p(num),
-                                          *(p(c) for c in cols)), "get_stats")
+        while True:
+            n = int(count.value)
+            slots = np.empty(n, np.uint32)
+            num = np.empty(n, np.int32)
+            cols = [np.empty(n, np.float32) for _ in range(5)]
+            N.check(L.nvrx_profiler_get_stats(self._h, n, ctypes.byref(count), p(slots), p(num),
+                                              *(p(c) for c in cols)), "get_stats")
+            if int(count.value) <= n:
+                break
+        sat = self.saturated()
+        if sat:
+            warnings.warn(f"{sat} captured kernel duration(s) above 4.29 s stored saturated at "
+                          "4294967295 ns", RuntimeWarning, stacklevel=2)
         names = [self._name_of(int(s)) for s in slots]
         return KernelSummaries(names, num, *cols)
 
@@ -259,3 +328,13 @@ class CuptiManager:
         """Feed kernel executions (e.g. from an external tracer) into the active run."""
         with self.lock:
             self.cupti_ext.push(name, durations_ns)
+
+    def register_kernel(self, name: str) -> int:
+        """Slot of a composite kernel name for ingest() records (valid until the next reset)."""
+        with self.lock:
+            return self.cupti_ext.register_kernel(name)
+
+    def ingest(self, records, stream=None):
+        """Device-resident {slot, ns} records from an external tracer into the active run."""
+        with self.lock:
+            self.cupti_ext.ingest(records, stream)

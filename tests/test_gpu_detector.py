@@ -43,21 +43,27 @@ def test_detector_single_rank_report():
         D.shutdown()
 
 
-def test_section_stats_torch_semantics():
+@pytest.mark.parametrize("lengths", [(1, 2, 3, 10, 1000, 8192),
+                                     # CustomSection.max_elapseds_len raised past the LDS path
+                                     (5, 16385, 40000, 0, 70001)])
+def test_section_stats_torch_semantics(lengths):
     import torch
 
     from nvidia_resiliency_ext.straggler import ops
 
     rng = np.random.default_rng(1)
-    secs = [rng.random(n) * 10 for n in (1, 2, 3, 10, 1000, 8192)]
+    secs = [rng.random(n) * 10 for n in lengths]
     off = np.zeros(len(secs) + 1, np.int64)
     off[1:] = np.cumsum([len(s) for s in secs])
     num, out = ops.section_stats(torch.from_numpy(np.concatenate(secs)).cuda(),
-                                 torch.from_numpy(off).cuda(), 8192)
+                                 torch.from_numpy(off).cuda(), max(lengths))
     out = out.cpu().numpy()
     for i, s in enumerate(secs):
         t = torch.tensor(s, dtype=torch.float64)
         assert num[i].item() == len(s)
+        if len(s) == 0:
+            assert np.all(np.isnan(out[:, i]))
+            continue
         assert out[0, i] == torch.min(t).item() and out[1, i] == torch.max(t).item()
         assert out[2, i] == torch.median(t).item()  # lower median, exact
         assert out[3, i] == pytest.approx(torch.mean(t).item(), rel=1e-14)

@@ -213,3 +213,98 @@ def test_records_stats_fused_matches_oracle(nslots, cap, lo, hi):
     miss = c[nslots:] != 0
     assert np.array_equal(miss, (num == 0).any(axis=0))
     assert np.array_equal(c[:nslots].view(np.float32)[~miss], want[~miss])
+
+
+def test_reset_renumbers_slots_across_intervals():
+    # a job that sees more distinct composite keys than nvrx_records_max_slots()
+    # over its lifetime (dynamic shapes) keeps reporting: reset forgets the kernels, as the
+    # reference's reset clears its map (CuptiProfiler.cpp:148-152)
+    maxs = int(cupti.N.lib().nvrx_records_max_slots())
+    per = maxs // 2 + 7
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=64)
+    try:
+        p.initialize()
+        p.start()
+        for window in range(3):  # 3 * per > maxs distinct names in all
+            names = [f"w{window}_k{i:05d}_blk_64_1_1_grid_{i % 13 + 1}_1_1" for i in range(per)]
+            slots = np.array([p.register_kernel(n) for n in names], np.uint32)
+            assert slots.min() == 0 and slots.max() == per - 1  # renumbered every interval
+            ns = (np.arange(per, dtype=np.uint32) + 1) * 1000
+            p.push_slots(np.repeat(slots, 2), np.repeat(ns, 2))
+            st = p.get_stats_columns()
+            assert st.names == sorted(names)
+            assert np.all(st.num == 2)
+            order = np.argsort(names)
+            np.testing.assert_array_equal(st.med, (ns[order] / 1000).astype(np.float32))
+            p.reset()
+            assert p.get_stats() == {}
+    finally:
+        p.close()
+
+
+def test_profiler_ingest_device_records():
+    # the device-side entry (SURVEY 8(b) nvrx_ingest_records): device {slot, ns} records land
+    # in the device log in push order after the host records staged before them
+    rng = np.random.default_rng(21)
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=100)
+    try:
+        p.initialize()
+        names = ["a_blk_1_1_1_grid_1_1_1", "b_blk_1_1_1_grid_1_1_1", "c_blk_1_1_1_grid_1_1_1"]
+        slots = [p.register_kernel(n) for n in names]
+        dev = torch.from_numpy(np.stack([np.full(5, slots[0], np.uint32),
+                                         np.arange(5, dtype=np.uint32) + 1], 1).view(np.int32)).cuda()
+        p.ingest(dev)  # stopped: ignored
+        p.start()
+        host_ns = rng.integers(1000, 90_000, size=80, dtype=np.uint32)
+        p.push(names[0], host_ns)
+        ing = np.stack([rng.integers(0, 3, size=300).astype(np.uint32),
+                        rng.integers(1000, 90_000, size=300, dtype=np.uint32)], 1)
+        ing[7, 0] = 3  # not a registered slot: not counted
+        p.ingest(torch.from_numpy(np.ascontiguousarray(ing).view(np.int32)).cuda())
+        st = p.get_stats()
+        for s, name in zip(slots, names):
+            d = ing[(ing[:, 0] == s), 1]
+            if s == slots[0]:
+                d = np.concatenate([host_ns, d])  # host records first: ring keeps the last 100
+            r = _oracle_slot_stats(d, 100)
+            got = st[name]
+            assert (got.num_calls, np.float32(got.min), np.float32(got.max), np.float32(got.median),
+                    np.float32(got.avg), np.float32(got.stddev)) == r, name
+        assert len(st) == 3
+    finally:
+        p.close()
+
+
+def test_profiler_drains_staged_records_at_the_watermark():
+    # bufferSize 8 KiB = 1024 records: pushes beyond it go to the device log right away
+    # (host memory bounded); the statistics are those of every record
+    p = cupti.KernelProfiler(bufferSize=8 * 1024, statsMaxLenPerKernel=8192)
+    try:
+        p.initialize()
+        p.start()
+        rng = np.random.default_rng(5)
+        all_ns = []
+        for _ in range(9):
+            d = rng.integers(1000, 500_000, size=700, dtype=np.uint32)
+            p.push("k_blk_1_1_1_grid_1_1_1", d)
+            all_ns.append(d)
+        slots, ns = p.get_records()
+        assert np.array_equal(ns, np.concatenate(all_ns))
+        r = _oracle_slot_stats(np.concatenate(all_ns), 8192)
+        s = p.get_stats()["k_blk_1_1_1_grid_1_1_1"]
+        assert (s.num_calls, np.float32(s.median), np.float32(s.avg)) == (r[0], r[3], r[4])
+    finally:
+        p.close()
+
+
+def test_profiler_saturates_durations_above_uint32_with_a_warning():
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=16)
+    try:
+        p.initialize()
+        p.start()
+        with pytest.warns(RuntimeWarning, match="saturated"):
+            p.push("slow_blk_1_1_1_grid_1_1_1", [5_000_000_000, 1000])
+        s = p.get_stats()["slow_blk_1_1_1_grid_1_1_1"]
+        assert s.max == np.float32(np.float32(4294967295) / np.float32(1000.0))
+    finally:
+        p.close()
