@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--report-every", type=int, default=20)
     ap.add_argument("--dump", default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--profiling-interval", type=int, default=1,
+                    help="Detector.initialize(profiling_interval=...): profile every k-th step")
     ap.add_argument("--profile-cuda", type=int, default=1,
                     help="0: sections time the CPU only (isolates the capture's cost)")
     a = ap.parse_args()
@@ -141,8 +143,8 @@ def main():
     t_base = timed(a.base_steps, step)
 
     D = straggler.Detector
-    D.initialize(scores_to_compute="all", gather_on_rank0=True, profiling_interval=1,
-                 report_time_interval=1e9)
+    D.initialize(scores_to_compute="all", gather_on_rank0=True,
+                 profiling_interval=a.profiling_interval, report_time_interval=1e9)
     prof = D.cupti_manager.cupti_ext
 
     def det_step():
@@ -219,7 +221,7 @@ def main():
             "n_gpus": ws, "capture": CAPTURE and cupti.capture_available(),
             "step_ms_without_detector": t_base * 1e3, "step_ms_with_detector": t_det * 1e3,
             "detector_overhead_pct": (t_det / t_base - 1) * 100,
-            "report_every_steps": a.report_every,
+            "report_every_steps": a.report_every, "profiling_interval": a.profiling_interval,
             "records_per_report": nrec, "kernel_keys": len(local_ks or {}),
             "report_ms": [x * 1e3 for x in t_rep],
             "report_ms_median": float(np.median(t_rep)) * 1e3,
