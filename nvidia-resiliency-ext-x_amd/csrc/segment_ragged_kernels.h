@@ -1,0 +1,404 @@
+// segment_ragged_kernels.h -- the length-class kernels of segment_ragged.hip, shared by the
+// translation units that instantiate them (segment_ragged*.hip: split so that the heavy
+// template instantiations -- 128-sample sorting networks, PL = 64/128 wave bodies -- compile
+// in parallel).  See segment_ragged.hip for the algorithm.
+#pragma once
+#include <algorithm>
+#include <mutex>
+
+#include "segment_kernels.h"
+
+namespace nvrx {
+namespace ragged {
+namespace {  // internal linkage: every translation unit keeps its own copy
+
+
+enum : int {
+    C_T8 = 0, C_T32, C_T64, C_T128,           // lane classes
+    C_W4, C_W8, C_W16, C_W32, C_W64, C_W128,  // wave classes (PL)
+    C_X,                                      // workgroup (EXACT kernel)
+    NCLASS
+};
+constexpr int CLS_THREADS = 1024;
+constexpr int CLS_MAX_BLOCKS = 1024;
+// segment lengths loaded per thread before any is classified: a block's chunk is tens of
+// thousands of segments, and one dependent load per 1024 of them left both passes
+// latency-bound (configs[3]: 153 + 118 us for 33.5 M segments)
+constexpr int CLS_BATCH = 8;
+
+// need = retained samples + misalignment slack a wave would have to hold
+__device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
+    if (n <= 8) return C_T8;
+    if (n <= 32) return C_T32;
+    if (n <= 64) return C_T64;
+    if (n <= 128) return C_T128;
+    if (exact) return C_X;
+    const int need = aligned16 ? n : n + 3;
+    if (need <= 64 * 4) return C_W4;
+    if (need <= 64 * 8) return C_W8;
+    if (need <= 64 * 16) return C_W16;
+    if (need <= 64 * 32) return C_W32;
+    if (need <= 64 * 64) return C_W64;
+    if (need <= 64 * 128) return C_W128;
+    return C_X;
+}
+
+// Wave-aggregated class counting: one LDS atomic per distinct class present in the
+// wave (leader = lowest lane); returns this lane's rank among same-class lanes plus the
+// class's previous count.  cls < 0: lane does not take part.
+__device__ __forceinline__ uint32_t wave_class_add(uint32_t* lcnt, int cls) {
+    uint64_t pending = __ballot(cls >= 0);
+    uint32_t mine = 0;
+    while (pending) {
+        const int leader = __builtin_ffsll(pending) - 1;
+        const int c = __builtin_amdgcn_readlane(cls, leader);
+        const uint64_t grp = __ballot(cls == c) & pending;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(&lcnt[c], (uint32_t)__popcll(grp));
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (cls == c) mine = base + mbcnt(grp);
+        pending &= ~grp;
+    }
+    return mine;
+}
+
+// pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
+__global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
+    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, uint32_t* bcnt,
+    nvrx_stats_soa out, ColRef cr) {
+    __shared__ uint32_t lcnt[NCLASS];
+    if (threadIdx.x < NCLASS) lcnt[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * chunk;
+    const int64_t hi = min(nseg, lo + chunk);
+    // per-lane class counters in registers (no LDS traffic per segment), one wave reduction
+    // and one LDS add per class at the end
+    unsigned mine[NCLASS];
+#pragma unroll
+    for (int c = 0; c < NCLASS; ++c) mine[c] = 0u;
+    for (int64_t b = lo; b < hi; b += CLS_THREADS * CLS_BATCH) {
+        int n[CLS_BATCH];
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            n[j] = s < hi ? segs.kept_len(s) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            if (n[j] == 0) {
+                write_empty(out, s);
+                cr.miss(s);
+            } else if (n[j] > 0) {  // n < 0: reduced elsewhere (or past the chunk)
+                const int cls = seg_class(n[j], aligned16 != 0, exact != 0);
+#pragma unroll
+                for (int c = 0; c < NCLASS; ++c) mine[c] += cls == c ? 1u : 0u;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NCLASS; ++c) {
+        const unsigned w = wave_sum_u32(mine[c]);
+        if (lane_id() == 0 && w) atomicAdd(&lcnt[c], w);
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLASS) bcnt[(int64_t)blockIdx.x * NCLASS + threadIdx.x] = lcnt[threadIdx.x];
+}
+
+// pass 2 (one block): boff[b][c] = start of class c + blocks before b; cls[c] = {start, count}
+__global__ __launch_bounds__(CLS_MAX_BLOCKS) void classify_scan_kernel(uint32_t* bcnt, int nblocks,
+                                                                       uint32_t* cls) {
+    __shared__ uint32_t wsum[CLS_MAX_BLOCKS / 64];
+    const int b = threadIdx.x;
+    const int w = b >> 6;
+    uint32_t start = 0;
+    for (int c = 0; c < NCLASS; ++c) {
+        const uint32_t v = b < nblocks ? bcnt[(int64_t)b * NCLASS + c] : 0u;
+        const uint32_t incl = wave_incl_scan_u32(v);
+        if (lane_id() == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int j = 0; j < CLS_MAX_BLOCKS / 64; ++j) {
+            before += j < w ? wsum[j] : 0u;
+            all += wsum[j];
+        }
+        if (b < nblocks) bcnt[(int64_t)b * NCLASS + c] = start + before + incl - v;
+        if (b == 0) {
+            cls[2 * c] = start;
+            cls[2 * c + 1] = all;
+        }
+        start += all;
+        __syncthreads();
+    }
+}
+
+// pass 3: scatter segment ids into the class-ordered list
+__global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
+    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, const uint32_t* boff,
+    uint32_t* list) {
+    __shared__ uint32_t lcnt[NCLASS];
+    __shared__ uint32_t lbase[NCLASS];
+    if (threadIdx.x < NCLASS) {
+        lcnt[threadIdx.x] = 0u;
+        lbase[threadIdx.x] = boff[(int64_t)blockIdx.x * NCLASS + threadIdx.x];
+    }
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * chunk;
+    const int64_t hi = min(nseg, lo + chunk);
+    for (int64_t b = lo; b < hi; b += CLS_THREADS * CLS_BATCH) {
+        int n[CLS_BATCH];
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            n[j] = s < hi ? segs.kept_len(s) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < CLS_BATCH; ++j) {  // the same order as the counting pass
+            const int64_t s = b + j * CLS_THREADS + threadIdx.x;
+            const int cls = n[j] > 0 ? seg_class(n[j], aligned16 != 0, exact != 0) : -1;
+            const uint32_t r = wave_class_add(lcnt, cls);
+            if (cls >= 0) list[lbase[cls] + r] = (uint32_t)s;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- lane classes
+template <int N>
+struct LaneOcc {
+    static constexpr int W = N >= 128 ? 2 : N >= 64 ? 4 : N >= 32 ? 6 : 8;
+};
+
+// Segments per lane per step: each takes a chain of three dependent loads (list entry,
+// descriptor, samples), so the shortest class runs B chains side by side.
+template <int N>
+struct LaneBatch {
+    static constexpr int B = N <= 8 ? 4 : 1;  // 2 for N = 32: 189 -> 214 us (configs[3])
+};
+
+// One lane per segment of 1..N samples.  u32 -> f32 us is monotone, so sorting the
+// integer ns sorts the floats computeStats sorts; then CuptiProfiler.cpp:53-71.
+template <int N>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LaneOcc<N>::W)))
+void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
+                           int aligned16, nvrx_stats_soa out, ColRef cr) {
+    constexpr int B = LaneBatch<N>::B;
+    // 32-bit list indices (a 64-bit loop cost lane<8> 315 -> 372 us); the host keeps the
+    // segment count below 2^32 - 2^26, so i + B * G never wraps
+    const uint32_t start = cls[0], cnt = cls[1];
+    const uint32_t G = gridDim.x * 256u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < cnt; i += B * G) {
+        int64_t s[B];
+        const uint32_t* p[B];
+        int n[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) s[b] = i + b * G < cnt ? (int64_t)list[start + i + b * G] : -1;
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            n[b] = 0;
+            p[b] = nullptr;
+            if (s[b] >= 0) segs.get(s[b], p[b], n[b]);  // 1 <= n <= N
+        }
+        unsigned v[B][N];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if (aligned16) {
+                const u32x4* q = (const u32x4*)p[b];
+#pragma unroll
+                for (int j = 0; j < N / 4; ++j) {
+                    u32x4 w = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+                    if (4 * j < n[b]) w = q[j];
+                    v[b][4 * j + 0] = w.x;
+                    v[b][4 * j + 1] = w.y;
+                    v[b][4 * j + 2] = w.z;
+                    v[b][4 * j + 3] = w.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < N; ++j) v[b][j] = j < n[b] ? p[b][j] : 0xFFFFFFFFu;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+            if (s[b] >= 0) lane_stats<N>(v[b], n[b], s[b], out, cr);
+    }
+}
+
+// ---------------------------------------------------------------- wave / workgroup classes
+// One wave per segment over a class list.  Waves take chunks of CH consecutive list
+// entries (static round robin; CH shrinks when the class is small so every wave gets
+// work); lanes 0..CH-1 fetch the chunk's segment descriptors in one coalesced access, so
+// per segment the only dependent memory access is the data itself -- and for PL <= 16
+// (short segments, few registers) the next segment's loads are issued before the
+// current one is reduced.
+template <int PL>
+struct ListPrefetch {
+    static constexpr bool on = PL <= 16;
+};
+template <int PL>
+struct ListOcc {  // the prefetch buffer costs PL more VGPRs
+    static constexpr int W = PL == 16 ? 6 : OccV<PL, false>::W;
+};
+constexpr int LIST_CHUNK = 16;
+
+template <int PL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ListOcc<PL>::W)))
+void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
+                           nvrx_stats_soa out, ColRef cr) {
+    constexpr int NB = Bins<PL>::NB;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id();
+    unsigned* hist = lds_hist + wave * NB;
+    const uint32_t start = cls[0], cnt = cls[1];
+    const uint32_t G = gridDim.x * 4u;
+    const uint32_t CH = max(1u, min((uint32_t)LIST_CHUNK, cnt / (4u * G)));
+    for (uint32_t c0 = (blockIdx.x * 4u + wave) * CH; c0 < cnt; c0 += G * CH) {
+        const int m = (int)min(CH, cnt - c0);
+        uint32_t sid = 0, plo = 0, phi = 0;
+        int nn = 0;
+        if (lane < m) {
+            sid = list[start + c0 + lane];
+            const uint32_t* p;
+            segs.get(sid, p, nn);
+            plo = (uint32_t)(uintptr_t)p;
+            phi = (uint32_t)((uintptr_t)p >> 32);
+        }
+        auto desc = [&](int j, int64_t& s, const uint32_t*& p, int& n) {
+            s = (uint32_t)__builtin_amdgcn_readlane((int)sid, j);
+            p = (const uint32_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)phi, j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)plo, j));
+            n = __builtin_amdgcn_readlane(nn, j);
+        };
+        int64_t s;
+        const uint32_t* p;
+        int n;
+        desc(0, s, p, n);
+        unsigned v[PL];
+        if (ListPrefetch<PL>::on) {
+            issue_loads<PL>(p, n, v);
+            for (int j = 0; j < m; ++j) {
+                // unconditional prefetch (the last one re-reads the current segment): a load
+                // under a branch would make the waitcnt at the join cover it
+                int64_t s2;
+                const uint32_t* p2;
+                int n2;
+                desc(j + 1 < m ? j + 1 : j, s2, p2, n2);
+                unsigned w[PL];
+                issue_loads<PL>(p2, n2, w);
+                int m0;
+                unsigned x0;
+                finish_loads<PL, false>(p, n, v, m0, x0);
+                fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+#pragma unroll
+                for (int i = 0; i < PL; ++i) v[i] = w[i];
+                s = s2;
+                p = p2;
+                n = n2;
+            }
+        } else {
+            for (int j = 0; j < m; ++j) {
+                if (j) desc(j, s, p, n);
+                int m0;
+                unsigned x0;
+                load_segment<PL, false>(p, n, v, m0, x0);
+                fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+            }
+        }
+    }
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(256) void seg_stats_exact_list_kernel(RaggedSegs segs,
+                                                                   const uint32_t* list,
+                                                                   const uint32_t* cls,
+                                                                   nvrx_stats_soa out, ColRef cr) {
+    __shared__ __attribute__((aligned(16))) float sbuf[NMAX];
+    const uint32_t start = cls[0], cnt = cls[1];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const int64_t s = list[start + i];
+        const uint32_t* p;
+        int n;
+        segs.get(s, p, n);
+        exact_body<NMAX>(p, n, s, sbuf, out, cr);
+    }
+}
+
+int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n <= 0)
+            n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+// Stream-ordered scratch from the device's default pool; the pool keeps freed blocks
+// (release threshold raised once) so steady-state reports do not return to the driver.
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+    static std::once_flag once[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        std::call_once(once[dev], [dev] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t thr = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+        });
+    }
+    return hipMallocAsync(p, bytes, st);
+}
+
+template <int N>
+void launch_lane(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls, bool aligned16,
+                 const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+    const unsigned blocks = (unsigned)(cu_count() * 2 * LaneOcc<N>::W);
+    hipLaunchKernelGGL((seg_stats_lane_kernel<N>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
+                       aligned16 ? 1 : 0, out, cr);
+}
+
+template <int PL>
+void launch_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                 const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+    const unsigned blocks = (unsigned)(cu_count() * ListOcc<PL>::W);
+    hipLaunchKernelGGL((seg_stats_list_kernel<PL>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
+                       out, cr);
+}
+
+hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                             int64_t max_len, const nvrx_stats_soa& out, const ColRef& cr,
+                             hipStream_t st) {
+    const unsigned cus = (unsigned)cu_count();
+    if (max_len <= 1024)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<1024>), dim3(cus * 8), dim3(256), 0, st, segs,
+                           list, cls, out, cr);
+    else if (max_len <= 8192)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<8192>), dim3(cus * 4), dim3(256), 0, st, segs,
+                           list, cls, out, cr);
+    else if (max_len <= NVRX_MAX_SEGMENT)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<NVRX_MAX_SEGMENT>), dim3(cus), dim3(256), 0,
+                           st, segs, list, cls, out, cr);
+    else
+        return hipErrorInvalidValue;
+    return hipSuccess;
+}
+
+
+}  // namespace
+}  // namespace ragged
+
+// per-class launches, each defined in the translation unit that instantiates its kernel
+void ragged_launch_lane(int n, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                        bool aligned16, const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st);
+void ragged_launch_list(int pl, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                        const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st);
+hipError_t ragged_launch_exact(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                               int64_t max_len, const nvrx_stats_soa& out, const ColRef& cr,
+                               hipStream_t st);
+
+}  // namespace nvrx
