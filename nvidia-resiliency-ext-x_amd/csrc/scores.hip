@@ -143,35 +143,57 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
     const bool do_ind = a.hist != nullptr;
     double swr = 0.0, wr = 0.0, nr = 0.0, swi = 0.0, wi = 0.0, ni = 0.0;
     bool zero_med = false;
-    const int32_t* num = a.num + r * K;
-    const T* med = (const T*)a.med + r * K;
-    const T* avg = (const T*)a.avg + r * K;
+    const int32_t* __restrict__ num = a.num + r * K;
+    const T* __restrict__ med = (const T*)a.med + r * K;
+    const T* __restrict__ avg = (const T*)a.avg + r * K;
     T* hist = (T*)a.hist;
-    for (int64_t k = tid; k < K; k += 256) {
-        if (a.col_valid && !a.col_valid[k]) continue;  // "ncclDev" filter (reporting.py:330-336)
-        const int32_t nm = num[k];
-        if (nm <= 0) continue;  // kernel not in this rank's summaries
-        const T mt = med[k];
-        const double m = (double)mt;
-        const double w = (double)nm * (double)avg[k];  // NUM * AVG (reporting.py:248)
-        if (do_ind) {
-            T* hp = hist + r * hs + (a.hist_index ? a.hist_index[k] : k);
-            const T h = tmin(*hp, mt);  // min(hist, MED) (reporting.py:310)
-            *hp = h;
-            zero_med |= (m == 0.0);
-            const double sc = (double)h / m;
-            const double t = sc * w;
-            swi = swi + t;
-            wi = wi + w;
-            ni += 1.0;
+    // Elements are taken SC at a time per thread, every load of a batch issued before any
+    // is used (one memory latency per batch instead of one per element: at R = 64 one row per
+    // workgroup is only 256 waves, so the kernel is latency-bound).  Each thread still visits
+    // k = tid, tid + 256, ... in increasing order, so the sums are the ones of the
+    // element-at-a-time loop, bit for bit.
+    constexpr int SC = 8;
+    for (int64_t k0 = tid; k0 < K; k0 += 256 * SC) {
+        int32_t nm[SC];
+        T mt[SC], av[SC], hv[SC];
+        float rf[SC];
+        bool ok[SC], rok[SC];
+#pragma unroll
+        for (int c = 0; c < SC; ++c) {
+            const int64_t k = k0 + c * 256;
+            const bool in = k < K;
+            nm[c] = in ? num[k] : 0;
+            ok[c] = in && (!a.col_valid || a.col_valid[k]);  // "ncclDev" filter (reporting.py:330-336)
+            mt[c] = in ? med[k] : (T)1;
+            av[c] = in ? avg[k] : (T)0;
+            hv[c] = (in && do_ind) ? hist[r * hs + (a.hist_index ? a.hist_index[k] : k)] : (T)0;
+            rf[c] = -1.0f;
+            rok[c] = false;
+            if (in && do_rel) {
+                const int64_t ri = a.ref_index ? a.ref_index[k] : k;
+                rf[c] = a.ref[ri];
+                rok[c] = !(a.ref_missing && a.ref_missing[ri]);
+            }
         }
-        if (do_rel) {
-            const int64_t ri = a.ref_index ? a.ref_index[k] : k;
-            const float rf = a.ref[ri];
-            const bool missing = a.ref_missing && a.ref_missing[ri];
-            if (rf >= 0.0f && !missing) {  // -1 sentinel / NaN => no reference (reporting.py:290, 244-245)
+#pragma unroll
+        for (int c = 0; c < SC; ++c) {
+            const int64_t k = k0 + c * 256;
+            if (!ok[c] || nm[c] <= 0) continue;  // kernel not in this rank's summaries
+            const double m = (double)mt[c];
+            const double w = (double)nm[c] * (double)av[c];  // NUM * AVG (reporting.py:248)
+            if (do_ind) {
+                const T h = tmin(hv[c], mt[c]);  // min(hist, MED) (reporting.py:310)
+                hist[r * hs + (a.hist_index ? a.hist_index[k] : k)] = h;
                 zero_med |= (m == 0.0);
-                const double sc = (double)rf / m;
+                const double sc = (double)h / m;
+                const double t = sc * w;
+                swi = swi + t;
+                wi = wi + w;
+                ni += 1.0;
+            }
+            if (do_rel && rf[c] >= 0.0f && rok[c]) {  // -1 / NaN => no reference (reporting.py:290, 244-245)
+                zero_med |= (m == 0.0);
+                const double sc = (double)rf[c] / m;
                 const double t = sc * w;
                 swr = swr + t;
                 wr = wr + w;
