@@ -92,3 +92,13 @@ def test_dist_utils_single_process_is_local():
     assert t.item() == 3.0
     assert du.gather_on_rank0(t)[0] is t
     assert du.is_all_true(False) is False and du.all_gather_object(5) == [5]
+
+
+def test_detection_section_fails_if_not_initialized():
+    # test_det_section_api.py:42-46 (no GPU needed: checked before anything is profiled)
+    from nvidia_resiliency_ext import straggler
+
+    assert not straggler.Detector.initialized
+    with pytest.raises(RuntimeError):
+        with straggler.Detector.detection_section("section00"):
+            pass
