@@ -234,11 +234,24 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
         lane_sums_f64<PL>(v, sdl, sql);
     const double sd = wave_sum_f64((double)sdl);  // exact: integer-valued, < 2^53
     const double sq = wave_sum_f64(sql);
+    // PADSKIP: the padding (d = 0, bin 0 at every level whose window starts at 0) is counted
+    // by the bin's initial value instead of one atomic per padding slot -- those atomics all
+    // hit one LDS word, a same-address serialisation.  Lane L's register i holds slot
+    // e = 256 (i >> 2) + (i & 3) + 4 L - m0.  Measured on configs[3]'s ragged classes
+    // (tools/gpu_ab_padskip.sh): PL 16 / 32 / 64 -12 / -25 / -16 %; PL 4 / 8 +3 % (little
+    // padding contention to remove), PL 128 +25 % (register pressure): kept for 16..64.
+    constexpr bool PADSKIP = !FULL && PL >= 16 && PL <= 64;
+    const unsigned pad_bin0 = PADSKIP ? (unsigned)pad : 0u;
+    const int eb = 4 * lane - m0;
+    const auto real = [&](int i) {
+        return !PADSKIP || (unsigned)(eb + 256 * (i >> 2) + (i & 3)) < (unsigned)n;
+    };
 #pragma unroll
-    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = (lane == 0 && j == 0) ? pad_bin0 : 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < PL; ++i) atomicAdd(&hist[v[i] >> shift], 1u);
+    for (int i = 0; i < PL; ++i)
+        if (real(i)) atomicAdd(&hist[v[i] >> shift], 1u);
     __builtin_amdgcn_wave_barrier();
 
     // ---- median: radix select on d = x - MIN ----
@@ -248,14 +261,15 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
     unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
     for (int level = 0;; ++level) {
         if (level > 0) {
+            const unsigned pad0 = wlo == 0 ? pad_bin0 : 0u;
 #pragma unroll
-            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = (lane == 0 && j == 0) ? pad0 : 0u;
             __builtin_amdgcn_wave_barrier();
             const unsigned span = (unsigned)NB << shift;  // level > 0: fits in 32 bits
 #pragma unroll
             for (int i = 0; i < PL; ++i) {
                 const unsigned q = v[i] - wlo;  // wraps for d < wlo
-                if (q < span) atomicAdd(&hist[q >> shift], 1u);
+                if (q < span && real(i)) atomicAdd(&hist[q >> shift], 1u);
             }
             __builtin_amdgcn_wave_barrier();
         }
