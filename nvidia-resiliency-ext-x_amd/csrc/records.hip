@@ -91,8 +91,13 @@ __device__ __forceinline__ void for_pairs(const u32x4* q, int64_t p_lo, int64_t 
     for (; i < p_hi; i += 64) f(q[i], i);
 }
 
-template <int RB_WAVES>
-__global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
+// RB_REGS > 0: the next RB_REGS pairs per lane after the LDS stash are also kept, in VGPRs
+// (64 x 16 B per lane: with one 4-wave block per CU, a wave owns its SIMD's register file),
+// so pass 2 re-reads only what neither holds -- nothing on configs[3] -- and pass 1 keeps
+// RB_REGS loads per lane in flight at once.
+template <int RB_WAVES, int RB_REGS>
+__global__ __launch_bounds__(64 * RB_WAVES) __attribute__((amdgpu_waves_per_eu(1, RB_REGS > 0 ? 1 : 8)))
+void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
     int32_t* counts, int64_t stash_pairs, int interleave) {
@@ -121,6 +126,10 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     const int64_t snp = wpairs ? min((hi - lo) >> 1, stash_pairs) : 0;
     u32x4* wstash = stash + wave * stash_pairs;
     const u32x4* wq = (const u32x4*)(rs + lo);
+    // pairs [snp, held) of the chunk are held in registers; records from lo + 2 held re-read
+    const int64_t np = wpairs ? (hi - lo) >> 1 : 0;
+    const int64_t held = wpairs ? min(np, snp + 64 * (int64_t)RB_REGS) : 0;
+    u32x4 reg[RB_REGS > 0 ? RB_REGS : 1];
 
     for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
         cnt[s] = 0u;
@@ -131,12 +140,26 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
     const auto count = [&](const nvrx_record& r) {
         if (r.slot < (uint32_t)nslots) atomicAdd(&cnt[r.slot], 1u);
     };
+    if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
+#pragma unroll
+        for (int u = 0; u < RB_REGS; ++u) {
+            const int64_t p = snp + lane + 64 * u;
+            reg[u] = p < held ? __builtin_nontemporal_load(wq + p) : u32x4{~0u, 0u, ~0u, 0u};
+        }
+    }
     for_pairs(wq, 0, snp, lane, [&](const u32x4& w, int64_t p) {
         wstash[p] = w;
         count(nvrx_record{w.x, w.y});
         count(nvrx_record{w.z, w.w});
     });
-    for_records(rs, lo + 2 * snp, hi, lane, wpairs, count);
+    if (RB_REGS > 0) {
+#pragma unroll
+        for (int u = 0; u < RB_REGS; ++u) {
+            count(nvrx_record{reg[u].x, reg[u].y});
+            count(nvrx_record{reg[u].z, reg[u].w});
+        }
+    }
+    for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, count);
     __syncthreads();
 
     // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
@@ -207,11 +230,17 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
             place(nvrx_record{w.z, w.w});
         }
     };
+    if (RB_REGS > 0) {  // no memory dependency: their atomics and stores go out first
+#pragma unroll
+        for (int u = 0; u < RB_REGS; ++u) {
+            place(nvrx_record{reg[u].x, reg[u].y});
+            place(nvrx_record{reg[u].z, reg[u].w});
+        }
+    }
     if (snp > 0 && interleave) {
-        const int64_t np = (hi - lo) >> 1;
-        const int64_t iters = (np - snp) / (64 * RB_UNROLL);
+        const int64_t iters = (np - held) / (64 * RB_UNROLL);
         const int per_it = iters > 0 ? (int)((snp / 64 + iters - 1) / iters) : 0;
-        int64_t i = snp + lane;
+        int64_t i = held + lane;
         for (; i + 64 * (RB_UNROLL - 1) < np; i += 64 * RB_UNROLL) {
             u32x4 w[RB_UNROLL];
 #pragma unroll
@@ -231,7 +260,7 @@ __global__ __launch_bounds__(64 * RB_WAVES) void records_bucket_kernel(
         place_stash(1 << 30);
     } else {
         place_stash(1 << 30);
-        for_records(rs, lo + 2 * snp, hi, lane, wpairs, place);
+        for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, place);
     }
     if (!any_ovf) return;
     __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
@@ -275,6 +304,7 @@ int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
 // dynamic LDS of a bucketing launch: a single workgroup may take the whole 160 KiB of a CU
 // (MI355X_MICROARCH.md), less the kernel's few static bytes
 constexpr size_t RB_LAUNCH_LDS = 160 * 1024 - 256;
+constexpr int RB_REGS_PAIRS = 64;  // register-held pairs per lane (256 VGPRs)
 
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
@@ -301,17 +331,19 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     size_t lds_launch = lds;
     if (bpc > 0) lds_launch = std::max(lds, (size_t)(160 * 1024) / (size_t)bpc - 1024);
     if (lds_launch > RB_LAUNCH_LDS) lds_launch = std::max(lds, RB_LAUNCH_LDS);
-    const void* fn = waves == 4    ? (const void*)records_bucket_kernel<4>
-                     : waves == 8 ? (const void*)records_bucket_kernel<8>
-                                  : (const void*)records_bucket_kernel<16>;
-    static bool attr_set[3] = {false, false, false};
-    const int wi = waves == 4 ? 0 : waves == 8 ? 1 : 2;
-    if (!attr_set[wi]) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)RB_LAUNCH_LDS);
-        if (e != hipSuccess) return e;
-        attr_set[wi] = true;
-    }
+    // register stash (RB_REGS_PAIRS pairs per lane, 4-wave blocks at one per CU;
+    // NVRX_RB_REGS=0 disables)
+    static const bool use_regs = [] {
+        const char* e = getenv("NVRX_RB_REGS");
+        return !(e && atoi(e) == 0);
+    }();
+    static bool attr_set[4] = {false, false, false, false};
+    const auto prep = [&](const void* fn, int idx) {
+        if (attr_set[idx]) return hipSuccess;
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
+        if (e == hipSuccess) attr_set[idx] = true;
+        return e;
+    };
     // The LDS that the padding leaves over holds the head of every wave's chunk from pass 1
     // to pass 2 (a whole number of 64-pair wave loads per wave; NVRX_RB_STASH=0 disables).
     static const bool use_stash = [] {
@@ -328,18 +360,31 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
         stash_pairs = (int64_t)((lds_launch - counters) / (16 * (size_t)waves)) & ~(int64_t)63;
     if (counters + (size_t)waves * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
     const dim3 grid((unsigned)nstreams), block(64 * waves);
-    if (waves == 4)
-        hipLaunchKernelGGL(records_bucket_kernel<4>, grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
-                           stash_interleave);
-    else if (waves == 8)
-        hipLaunchKernelGGL(records_bucket_kernel<8>, grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
-                           stash_interleave);
-    else
-        hipLaunchKernelGGL(records_bucket_kernel<16>, grid, block, lds_launch, st, recs, rec_off,
+    // one 4-wave block per CU: its waves may take whole SIMD register files (short streams
+    // only predicate the register loads off)
+    const bool regs = use_regs && waves == 4 && bpc == 1;
+    hipError_t e;
+    if (waves == 4 && regs) {
+        if ((e = prep((const void*)records_bucket_kernel<4, RB_REGS_PAIRS>, 3)) != hipSuccess) return e;
+        hipLaunchKernelGGL((records_bucket_kernel<4, RB_REGS_PAIRS>), grid, block, lds_launch, st, recs, rec_off,
                            nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
                            stash_interleave);
+    } else if (waves == 4) {
+        if ((e = prep((const void*)records_bucket_kernel<4, 0>, 0)) != hipSuccess) return e;
+        hipLaunchKernelGGL((records_bucket_kernel<4, 0>), grid, block, lds_launch, st, recs, rec_off, nslots,
+                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
+                           stash_interleave);
+    } else if (waves == 8) {
+        if ((e = prep((const void*)records_bucket_kernel<8, 0>, 1)) != hipSuccess) return e;
+        hipLaunchKernelGGL((records_bucket_kernel<8, 0>), grid, block, lds_launch, st, recs, rec_off, nslots,
+                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
+                           stash_interleave);
+    } else {
+        if ((e = prep((const void*)records_bucket_kernel<16, 0>, 2)) != hipSuccess) return e;
+        hipLaunchKernelGGL((records_bucket_kernel<16, 0>), grid, block, lds_launch, st, recs, rec_off,
+                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
+                           stash_interleave);
+    }
     return hipGetLastError();
 }
 
