@@ -92,11 +92,11 @@ __device__ __forceinline__ void for_pairs(const u32x4* q, int64_t p_lo, int64_t 
 }
 
 // RB_REGS > 0: the next RB_REGS pairs per lane after the LDS stash are also kept, in VGPRs
-// (64 x 16 B per lane: with one 4-wave block per CU, a wave owns its SIMD's register file),
-// so pass 2 re-reads only what neither holds -- nothing on configs[3] -- and pass 1 keeps
-// RB_REGS loads per lane in flight at once.
+// (16 B each; with one block per CU the block may take a SIMD register file's worth per
+// SIMD), so pass 2 re-reads only what neither holds -- nothing on configs[3] -- and pass 1
+// has RB_REGS loads per lane in flight at once.
 template <int RB_WAVES, int RB_REGS>
-__global__ __launch_bounds__(64 * RB_WAVES) __attribute__((amdgpu_waves_per_eu(1, RB_REGS > 0 ? 1 : 8)))
+__global__ __launch_bounds__(64 * RB_WAVES) __attribute__((amdgpu_waves_per_eu(1, RB_REGS > 32 ? 1 : RB_REGS > 16 ? 2 : RB_REGS > 0 ? 4 : 8)))
 void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
@@ -304,7 +304,28 @@ int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
 // dynamic LDS of a bucketing launch: a single workgroup may take the whole 160 KiB of a CU
 // (MI355X_MICROARCH.md), less the kernel's few static bytes
 constexpr size_t RB_LAUNCH_LDS = 160 * 1024 - 256;
-constexpr int RB_REGS_PAIRS = 64;  // register-held pairs per lane (256 VGPRs)
+// register-held record pairs per block, whatever the wave count: 16,384 pairs = 256 KiB =
+// 64 KiB per SIMD (half its register file) -- 4 waves x 64 pairs per lane (256 VGPRs),
+// 8 x 32 or 16 x 16 (64 VGPRs)
+constexpr int RB_REGS_PER_BLOCK = 16384;
+
+template <int W, int REGS>
+static hipError_t launch_bucket(int64_t nstreams, size_t lds_launch, hipStream_t st, const nvrx_record* recs,
+                                const int64_t* rec_off, int64_t nslots, int64_t cap, int force_stable,
+                                int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
+                                int64_t stash_pairs, int interleave) {
+    static bool attr_set = false;  // per instantiation
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel<W, REGS>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((records_bucket_kernel<W, REGS>), dim3((unsigned)nstreams), dim3(64 * W), lds_launch,
+                       st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts,
+                       stash_pairs, interleave);
+    return hipGetLastError();
+}
 
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
@@ -312,40 +333,36 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     if (nstreams <= 0 || nslots <= 0) return hipSuccess;
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
-    // Streams resident at once = blocks per CU x CUs.  One block per CU keeps the resident
-    // streams (read twice) and their bucket outputs (scattered 4-B writes) inside the
-    // 256 MB Infinity Cache: the second pass then reads from it and partial lines merge
-    // there instead of in HBM (configs[3] on MI355X: 5.6 ms with 6 blocks/CU -> 4.4 ms with
-    // one 4-wave block; 16-wave blocks contend on the shared LDS counters).
-    // NVRX_RB_WAVES (4 | 8 | 16) and NVRX_RB_BPC (blocks per CU, 0 = as many as fit) select
-    // the shape for A/B; LDS padding enforces the per-CU limit.
-    static const int waves = [] {
-        const char* e = getenv("NVRX_RB_WAVES");
-        const int w = e ? atoi(e) : 4;
-        return (w == 8 || w == 16) ? w : 4;
+    // Streams resident at once = blocks per CU x CUs.  One block per CU (LDS padding) keeps
+    // the resident streams and their bucket outputs (scattered 4-B writes) inside the 256 MB
+    // Infinity Cache, where partial lines merge (configs[3]: 5.6 ms with 6 blocks/CU -> 4.4 ms
+    // with one, round 1).  That block holds a whole configs[3] stream between the passes:
+    // its LDS stash (~136 KiB) plus RB_REGS_PER_BLOCK register pairs (64 KiB), so pass 2
+    // reads nothing back.  Pass 2 is LDS-atomic latency bound: 16 waves x 16 register pairs
+    // (4 waves per SIMD) beat 8 x 32 and 4 x 64 (configs[3] statistics 5.25 / 5.31 / 5.51 ms,
+    // tools/gpu_ab_waves_regs.sh); without register pairs 16-wave blocks lost to 4 (round 1).
+    // A/B knobs: NVRX_RB_WAVES (4 | 8 | 16), NVRX_RB_BPC (blocks per CU, 0 = as many as fit),
+    // NVRX_RB_REGS=0 (no register pairs), NVRX_RB_STASH (0 = no LDS stash, 1 = not interleaved).
+    static const bool use_regs = [] {
+        const char* e = getenv("NVRX_RB_REGS");
+        return !(e && atoi(e) == 0);
     }();
     static const int bpc = [] {
         const char* e = getenv("NVRX_RB_BPC");
         return e ? atoi(e) : 1;
     }();
+    const bool regs = use_regs && bpc == 1;
+    static const int waves_env = [] {
+        const char* e = getenv("NVRX_RB_WAVES");
+        const int w = e ? atoi(e) : 0;
+        return (w == 4 || w == 8 || w == 16) ? w : 0;
+    }();
+    const int waves = waves_env ? waves_env : regs ? 16 : 4;
     size_t lds_launch = lds;
     if (bpc > 0) lds_launch = std::max(lds, (size_t)(160 * 1024) / (size_t)bpc - 1024);
     if (lds_launch > RB_LAUNCH_LDS) lds_launch = std::max(lds, RB_LAUNCH_LDS);
-    // register stash (RB_REGS_PAIRS pairs per lane, 4-wave blocks at one per CU;
-    // NVRX_RB_REGS=0 disables)
-    static const bool use_regs = [] {
-        const char* e = getenv("NVRX_RB_REGS");
-        return !(e && atoi(e) == 0);
-    }();
-    static bool attr_set[4] = {false, false, false, false};
-    const auto prep = [&](const void* fn, int idx) {
-        if (attr_set[idx]) return hipSuccess;
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
-        if (e == hipSuccess) attr_set[idx] = true;
-        return e;
-    };
     // The LDS that the padding leaves over holds the head of every wave's chunk from pass 1
-    // to pass 2 (a whole number of 64-pair wave loads per wave; NVRX_RB_STASH=0 disables).
+    // to pass 2 (a whole number of 64-pair wave loads per wave).
     static const bool use_stash = [] {
         const char* e = getenv("NVRX_RB_STASH");
         return !(e && atoi(e) == 0);
@@ -359,33 +376,20 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     if (use_stash && lds_launch > counters)
         stash_pairs = (int64_t)((lds_launch - counters) / (16 * (size_t)waves)) & ~(int64_t)63;
     if (counters + (size_t)waves * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)nstreams), block(64 * waves);
-    // one 4-wave block per CU: its waves may take whole SIMD register files (short streams
-    // only predicate the register loads off)
-    const bool regs = use_regs && waves == 4 && bpc == 1;
-    hipError_t e;
-    if (waves == 4 && regs) {
-        if ((e = prep((const void*)records_bucket_kernel<4, RB_REGS_PAIRS>, 3)) != hipSuccess) return e;
-        hipLaunchKernelGGL((records_bucket_kernel<4, RB_REGS_PAIRS>), grid, block, lds_launch, st, recs, rec_off,
-                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
-                           stash_interleave);
-    } else if (waves == 4) {
-        if ((e = prep((const void*)records_bucket_kernel<4, 0>, 0)) != hipSuccess) return e;
-        hipLaunchKernelGGL((records_bucket_kernel<4, 0>), grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
-                           stash_interleave);
-    } else if (waves == 8) {
-        if ((e = prep((const void*)records_bucket_kernel<8, 0>, 1)) != hipSuccess) return e;
-        hipLaunchKernelGGL((records_bucket_kernel<8, 0>), grid, block, lds_launch, st, recs, rec_off, nslots,
-                           cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
-                           stash_interleave);
-    } else {
-        if ((e = prep((const void*)records_bucket_kernel<16, 0>, 2)) != hipSuccess) return e;
-        hipLaunchKernelGGL((records_bucket_kernel<16, 0>), grid, block, lds_launch, st, recs, rec_off,
-                           nslots, cap, force_stable, seg_off, seg_len, out_ns, counts, stash_pairs,
-                           stash_interleave);
+#define NVRX_RB_LAUNCH(W, REGS)                                                                      \
+    return launch_bucket<W, REGS>(nstreams, lds_launch, st, recs, rec_off, nslots, cap, force_stable, \
+                                  seg_off, seg_len, out_ns, counts, stash_pairs, stash_interleave)
+    if (waves == 16) {
+        if (regs) NVRX_RB_LAUNCH(16, RB_REGS_PER_BLOCK / (64 * 16));
+        NVRX_RB_LAUNCH(16, 0);
     }
-    return hipGetLastError();
+    if (waves == 8) {
+        if (regs) NVRX_RB_LAUNCH(8, RB_REGS_PER_BLOCK / (64 * 8));
+        NVRX_RB_LAUNCH(8, 0);
+    }
+    if (regs) NVRX_RB_LAUNCH(4, RB_REGS_PER_BLOCK / (64 * 4));
+    NVRX_RB_LAUNCH(4, 0);
+#undef NVRX_RB_LAUNCH
 }
 
 // Whole record-stream report statistics: bucketing, then length-classed statistics of

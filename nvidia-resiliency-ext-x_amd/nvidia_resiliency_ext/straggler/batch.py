@@ -67,7 +67,7 @@ class MatrixReporter:
     def __init__(self, R: int, K: int, *, cap: int = 8192, relative: bool = True,
                  individual: bool = True, thr_rel: float = 0.75, thr_ind: float = 0.75,
                  col_valid: Optional[torch.Tensor] = None, mode: int = ops.STATS_FAST,
-                 round_f32: bool = False, group=None, device=None):
+                 round_f32: bool = False, group=None, device=None, exchange: Optional[bool] = None):
         self.R, self.K, self.cap = R, K, cap
         self.relative, self.individual = relative, individual
         self.thr_rel, self.thr_ind = thr_rel, thr_ind
@@ -80,6 +80,11 @@ class MatrixReporter:
         if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
             self.world = torch.distributed.get_world_size(group)
             self.gloo = torch.distributed.get_backend(group) == torch.distributed.Backend.GLOO
+        # exchange: the multi-GPU scoring (partials -> all_gather -> finalize) even in a world
+        # of one -- how a one-GPU box runs the RCCL branch (tests); default: world > 1
+        self.exchange = self.world > 1 if exchange is None else bool(exchange)
+        if self.exchange and not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            raise RuntimeError("MatrixReporter(exchange=True) needs an initialized process group")
         self.stats = ops.SegmentStats.empty(R * K, d)
         self.col_valid = col_valid
         # per-kernel reference, produced by the stats kernel's epilogue: [min bits | missing]
@@ -88,7 +93,7 @@ class MatrixReporter:
         self.hist = torch.full((R, K), float("inf"), dtype=torch.float32, device=d) if individual else None
         self.partials = torch.empty((R, 6), dtype=torch.float64, device=d)
         self.gathered = (torch.empty((self.world, R, 6), dtype=torch.float64, device=d)
-                         if self.world > 1 else None)
+                         if self.exchange else None)
         # one packed result buffer -> one device-to-host copy per report:
         # [gpu_rel f64 R][gpu_ind f64 R][strag_rel u8 R][strag_ind u8 R][pad][err i32]
         self._e = (18 * R + 7) // 8 * 8
@@ -162,7 +167,7 @@ class MatrixReporter:
         self.err.zero_()
         ref = self.col_ref.view(torch.float32)[:K] if self.relative else None
         missing = self.col_ref[K:2 * K] if self.relative else None
-        if self.world == 1:
+        if not self.exchange:
             ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
                        ref_missing=missing, hist=self.hist, err=self.err,
                        finalize=self._outputs())
@@ -225,7 +230,7 @@ class ReportGraph:
         side.wait_stream(torch.cuda.current_stream(rep.device))
         with torch.cuda.stream(side):  # one eager pass: first-launch setup outside the capture
             rep.compute_stats(ns, s_push)
-            if rep.world == 1:
+            if not rep.exchange:
                 rep.compute_scores()
         torch.cuda.current_stream(rep.device).wait_stream(side)
         torch.cuda.synchronize(rep.device)
@@ -233,7 +238,7 @@ class ReportGraph:
         with torch.cuda.graph(self.stats):
             rep.compute_stats(ns, s_push)
         self.rest = self.full = None
-        if rep.world == 1:
+        if not rep.exchange:
             self.rest = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.rest):
                 rep.compute_scores()
