@@ -100,16 +100,19 @@ __global__ __launch_bounds__(64 * RB_WAVES) __attribute__((amdgpu_waves_per_eu(1
 void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
-    int32_t* counts, int64_t stash_pairs, int interleave) {
+    int32_t* counts, int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
     uint32_t* start = lds + 2 * nslots; // [nslots] bucket start (relative to stream base) | RB_OVF
+    // [stage_cap] the first bucket positions of the stream, assembled in LDS and written out
+    // with 16-byte stores (stage_cap: a multiple of 4, 0 = off)
+    uint32_t* stage = lds + ((3 * nslots + 3) & ~(int64_t)3);
     // [RB_WAVES][stash_pairs] record pairs: the head of every wave's chunk, kept from pass 1
     // for pass 2 (which would otherwise re-read them from the memory side)
-    u32x4* stash = (u32x4*)(lds + ((3 * nslots + 3) & ~(int64_t)3));
+    u32x4* stash = (u32x4*)(stage + stage_cap);
     __shared__ uint32_t any_ovf;
-    __shared__ uint32_t wtot[RB_WAVES];
+    __shared__ uint32_t wtot[RB_WAVES], wcold[RB_WAVES];
     const int64_t t = blockIdx.x;
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
@@ -165,35 +168,64 @@ void records_bucket_kernel(
     // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
     // block's other waves would otherwise wait at the barrier while one wave walks all the
     // slots: with one block per CU that wait was ~1 ms of configs[3]):
-    //   (a) chunk totals -> LDS, (b) each wave scans its chunk from the preceding totals
+    //   (a) chunk totals -> LDS, (b) each wave scans its chunk from the preceding totals.
+    // With staging the buckets of the cold slots (keep <= cold_max, not overflowed) come
+    // first, in slot order, then the others: two scans, the second carried past the cold
+    // total.  The cold region's first stage_cap positions are assembled in LDS and written out
+    // with 16-byte stores, the rest as before (see records_bucket for what pays).
     const auto keep_of = [&](uint32_t total) {
         return (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+    };
+    const bool staging = stage_cap > 0 && !force_stable;
+    const auto is_cold = [&](uint32_t total) {
+        const uint32_t keep = keep_of(total);
+        return staging && keep == total && keep <= cold_max;
     };
     const int64_t chunk = ((nslots + RB_WAVES - 1) / RB_WAVES + 63) & ~(int64_t)63;
     const int64_t c_lo = min(nslots, chunk * wave), c_hi = min(nslots, c_lo + chunk);
     {
-        uint32_t part = 0;
-        for (int64_t s = c_lo + lane; s < c_hi; s += 64) part += (keep_of(cnt[s]) + 3u) & ~3u;
+        uint32_t part = 0, partc = 0;
+        for (int64_t s = c_lo + lane; s < c_hi; s += 64) {
+            const uint32_t total = cnt[s];
+            const uint32_t padded = (keep_of(total) + 3u) & ~3u;
+            if (is_cold(total)) partc += padded;
+            else part += padded;
+        }
         part = wave_sum_u32(part);
-        if (lane == 0) wtot[wave] = part;
+        partc = wave_sum_u32(partc);
+        if (lane == 0) {
+            wtot[wave] = part;
+            wcold[wave] = partc;
+        }
     }
     __syncthreads();
+    uint32_t cold_total = 0;
     {
-        uint32_t carry = 0;
-        for (int w = 0; w < wave; ++w) carry += wtot[w];
+        uint32_t carry = 0, carryc = 0;
+        for (int w = 0; w < RB_WAVES; ++w) {
+            cold_total += wcold[w];
+            if (w < wave) {
+                carry += wtot[w];
+                carryc += wcold[w];
+            }
+        }
+        carry += cold_total;
         bool overflow = false;
         for (int64_t c = c_lo; c < c_hi; c += 64) {
             const int64_t s = c + lane;
             uint32_t keep = 0, total = 0;
+            bool cold = false;
             if (s < c_hi) {
                 total = cnt[s];
                 keep = keep_of(total);
+                cold = is_cold(total);
             }
             const bool ovf = keep != total;
             overflow |= ovf;
             const uint32_t padded = (keep + 3u) & ~3u;
-            const uint32_t incl = wave_incl_scan_u32(padded);
-            const uint32_t st = carry + incl - padded;
+            const uint32_t incl = wave_incl_scan_u32(cold ? 0u : padded);
+            const uint32_t inclc = wave_incl_scan_u32(cold ? padded : 0u);
+            const uint32_t st = cold ? carryc + inclc - padded : carry + incl - padded;
             if (s < c_hi) {
                 const uint32_t flag = ovf || force_stable ? RB_OVF : 0u;
                 start[s] = st | flag;
@@ -204,10 +236,14 @@ void records_bucket_kernel(
                 counts[g] = (int32_t)total;
             }
             carry += __builtin_amdgcn_readlane(incl, 63);
+            carryc += __builtin_amdgcn_readlane(inclc, 63);
         }
         if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
     }
     __syncthreads();
+    // positions below stage_lim go to LDS (cold buckets only: an overflowed slot's walk
+    // writes to memory directly)
+    const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
     uint32_t* out = out_ns + base;
 
     // records of slots that kept everything: any order.  The cursor starts at the bucket's
@@ -217,7 +253,10 @@ void records_bucket_kernel(
     const auto place = [&](const nvrx_record& r) {
         if (r.slot < (uint32_t)nslots) {
             const uint32_t pos = atomicAdd(&cur[r.slot], 1u);
-            if (!(pos & RB_OVF)) out[pos] = r.ns;
+            if (pos < stage_lim)
+                stage[pos] = r.ns;
+            else if (!(pos & RB_OVF))
+                out[pos] = r.ns;
         }
     };
     // The stashed head of the chunk (LDS) is placed while each batch of the rest's loads is
@@ -261,6 +300,12 @@ void records_bucket_kernel(
     } else {
         place_stash(1 << 30);
         for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, place);
+    }
+    if (stage_lim > 0) {  // the assembled head of the bucket array, in 16-byte stores
+        __syncthreads();
+        const u32x4* sv = (const u32x4*)stage;
+        u32x4* ov = (u32x4*)out;  // out = stream base: 16-byte aligned
+        for (uint32_t i = threadIdx.x; i < stage_lim / 4; i += blockDim.x) ov[i] = sv[i];
     }
     if (!any_ovf) return;
     __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
@@ -308,12 +353,14 @@ constexpr size_t RB_LAUNCH_LDS = 160 * 1024 - 256;
 // 64 KiB per SIMD (half its register file) -- 4 waves x 64 pairs per lane (256 VGPRs),
 // 8 x 32 or 16 x 16 (64 VGPRs)
 constexpr int RB_REGS_PER_BLOCK = 16384;
+constexpr int RB_STAGE_KB_DEFAULT = 96;  // LDS staging of the cold buckets
+constexpr int RB_COLD_DEFAULT = 512;     // largest cold bucket (records)
 
 template <int W, int REGS>
 static hipError_t launch_bucket(int64_t nstreams, size_t lds_launch, hipStream_t st, const nvrx_record* recs,
                                 const int64_t* rec_off, int64_t nslots, int64_t cap, int force_stable,
                                 int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
-                                int64_t stash_pairs, int interleave) {
+                                int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max) {
     static bool attr_set = false;  // per instantiation
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel<W, REGS>,
@@ -323,7 +370,7 @@ static hipError_t launch_bucket(int64_t nstreams, size_t lds_launch, hipStream_t
     }
     hipLaunchKernelGGL((records_bucket_kernel<W, REGS>), dim3((unsigned)nstreams), dim3(64 * W), lds_launch,
                        st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts,
-                       stash_pairs, interleave);
+                       stash_pairs, interleave, stage_cap, cold_max);
     return hipGetLastError();
 }
 
@@ -371,14 +418,28 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
         const char* e = getenv("NVRX_RB_STASH");
         return (e && atoi(e) == 1) ? 0 : 1;
     }();
+    // Staging (NVRX_RB_STAGE_KB of LDS, 0 = off; NVRX_RB_COLD = the largest cold bucket)
+    static const int64_t stage_kb = [] {
+        const char* e = getenv("NVRX_RB_STAGE_KB");
+        return (int64_t)(e ? atoi(e) : RB_STAGE_KB_DEFAULT);
+    }();
+    static const uint32_t cold_max = [] {
+        const char* e = getenv("NVRX_RB_COLD");
+        return (uint32_t)(e ? atoi(e) : RB_COLD_DEFAULT);
+    }();
     const size_t counters = (size_t)((3 * nslots + 3) & ~(int64_t)3) * sizeof(uint32_t);
+    int64_t stage_cap = 0;
+    if (lds_launch > counters)
+        stage_cap = std::min<int64_t>(stage_kb * 256, (int64_t)(lds_launch - counters) / 4) & ~(int64_t)3;
+    const size_t fixed = counters + (size_t)stage_cap * 4;
     int64_t stash_pairs = 0;
-    if (use_stash && lds_launch > counters)
-        stash_pairs = (int64_t)((lds_launch - counters) / (16 * (size_t)waves)) & ~(int64_t)63;
-    if (counters + (size_t)waves * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
+    if (use_stash && lds_launch > fixed)
+        stash_pairs = (int64_t)((lds_launch - fixed) / (16 * (size_t)waves)) & ~(int64_t)63;
+    if (fixed + (size_t)waves * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
 #define NVRX_RB_LAUNCH(W, REGS)                                                                      \
     return launch_bucket<W, REGS>(nstreams, lds_launch, st, recs, rec_off, nslots, cap, force_stable, \
-                                  seg_off, seg_len, out_ns, counts, stash_pairs, stash_interleave)
+                                  seg_off, seg_len, out_ns, counts, stash_pairs, stash_interleave, \
+                                  stage_cap, cold_max)
     if (waves == 16) {
         if (regs) NVRX_RB_LAUNCH(16, RB_REGS_PER_BLOCK / (64 * 16));
         NVRX_RB_LAUNCH(16, 0);
