@@ -181,8 +181,10 @@ typedef struct nvrx_record {
  * (CircularBuffer semantics; order inside a bucket is push order).  Outputs (device):
  *   seg_off [nstreams*nslots] int64, seg_len [nstreams*nslots] int32:
  *       bucket (t, s) = out_ns[seg_off[t*nslots+s] : + seg_len[t*nslots+s]]; every bucket
- *       starts 16-byte aligned, so it feeds nvrx_segment_stats_ragged(aligned16=1)
- *   out_ns  [>= nvrx_records_bucket_capacity(n, nstreams, nslots)] uint32
+ *       starts 16-byte aligned, so it feeds nvrx_segment_stats_ragged(aligned16=1); where a
+ *       stream's buckets lie inside its region is unspecified (slots with few records are
+ *       laid out first and assembled in LDS)
+ *   out_ns  [>= nvrx_records_bucket_capacity(n, nstreams, nslots)] uint32, 16-byte aligned
  *   counts  [nstreams*nslots] int32: total pushes per (stream, slot) on return */
 int64_t nvrx_records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots);
 int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,

@@ -198,6 +198,7 @@ int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t 
     NVRX_CHECK_ARG(mode == NVRX_STATS_FAST || mode == NVRX_STATS_EXACT,
                    "nvrx_records_stats: unknown mode");
     NVRX_CHECK_ARG(nstreams * nslots < (int64_t)1 << 31, "nvrx_records_stats: too many segments");
+    NVRX_CHECK_ARG(((uintptr_t)out_ns & 15) == 0, "nvrx_records_stats: out_ns not 16-byte aligned");
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
     NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT, "nvrx_records_stats: retained run longer than NVRX_MAX_SEGMENT");
     return hip_status(nvrx::records_stats(recs, rec_off, nstreams, nslots, cap, mode, max_len,
@@ -216,6 +217,7 @@ int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t
                        (rec_off && seg_off && seg_len && out_ns && counts),
                    "nvrx_records_bucket: null array");
     NVRX_CHECK_ARG(nstreams < (int64_t)1 << 31, "nvrx_records_bucket: too many streams");
+    NVRX_CHECK_ARG(((uintptr_t)out_ns & 15) == 0, "nvrx_records_bucket: out_ns not 16-byte aligned");
     return hip_status(nvrx::records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off,
                                            seg_len, out_ns, counts, S(stream)),
                       "nvrx_records_bucket");
