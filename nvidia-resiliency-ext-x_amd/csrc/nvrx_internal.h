@@ -37,7 +37,8 @@ hipError_t stragglers(const double* score, int64_t n, double thr, uint8_t* mask,
 int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots);
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
-                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st);
+                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
+                          const nvrx_stats_soa* tiny = nullptr);
 hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                          int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,

@@ -36,6 +36,7 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 }
 
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
+constexpr int RB_TINY = 8;  // records_stats: buckets this short are reduced by the bucketing kernel
 
 // records [lo, hi) of a stream in 16-byte pairs where the base allows it; f(rec) per record.
 // RB_UNROLL independent loads per lane are issued before any is consumed: a wave keeps
@@ -100,7 +101,8 @@ __global__ __launch_bounds__(64 * RB_WAVES) __attribute__((amdgpu_waves_per_eu(1
 void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
-    int32_t* counts, int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max) {
+    int32_t* counts, int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max,
+    nvrx_stats_soa tiny) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
@@ -112,7 +114,7 @@ void records_bucket_kernel(
     // for pass 2 (which would otherwise re-read them from the memory side)
     u32x4* stash = (u32x4*)(stage + stage_cap);
     __shared__ uint32_t any_ovf;
-    __shared__ uint32_t wtot[RB_WAVES], wcold[RB_WAVES];
+    __shared__ uint32_t wtot[3][RB_WAVES];
     const int64_t t = blockIdx.x;
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
@@ -169,74 +171,82 @@ void records_bucket_kernel(
     // block's other waves would otherwise wait at the barrier while one wave walks all the
     // slots: with one block per CU that wait was ~1 ms of configs[3]):
     //   (a) chunk totals -> LDS, (b) each wave scans its chunk from the preceding totals.
-    // With staging the buckets of the cold slots (keep <= cold_max, not overflowed) come
-    // first, in slot order, then the others: two scans, the second carried past the cold
-    // total.  The cold region's first stage_cap positions are assembled in LDS and written out
-    // with 16-byte stores, the rest as before (see records_bucket for what pays).
+    // With staging the bucket array is laid out by tier, slot order inside a tier: the tiny
+    // buckets (<= RB_TINY records), the other cold ones (<= cold_max, not overflowed), then
+    // the rest -- one scan per tier, each carried past the tiers before it.  The first
+    // stage_cap positions (tiny and cold buckets) are assembled in LDS and written out with
+    // 16-byte stores; see records_bucket for what pays.
     const auto keep_of = [&](uint32_t total) {
         return (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
     };
     const bool staging = stage_cap > 0 && !force_stable;
-    const auto is_cold = [&](uint32_t total) {
+    const auto tier_of = [&](uint32_t total) {
         const uint32_t keep = keep_of(total);
-        return staging && keep == total && keep <= cold_max;
+        if (!staging || keep != total || keep > cold_max) return 2;
+        return keep <= (uint32_t)RB_TINY ? 0 : 1;
     };
     const int64_t chunk = ((nslots + RB_WAVES - 1) / RB_WAVES + 63) & ~(int64_t)63;
     const int64_t c_lo = min(nslots, chunk * wave), c_hi = min(nslots, c_lo + chunk);
     {
-        uint32_t part = 0, partc = 0;
+        uint32_t p0 = 0, p1 = 0, p2 = 0;
         for (int64_t s = c_lo + lane; s < c_hi; s += 64) {
             const uint32_t total = cnt[s];
             const uint32_t padded = (keep_of(total) + 3u) & ~3u;
-            if (is_cold(total)) partc += padded;
-            else part += padded;
+            const int tr = tier_of(total);
+            p0 += tr == 0 ? padded : 0u;
+            p1 += tr == 1 ? padded : 0u;
+            p2 += tr == 2 ? padded : 0u;
         }
-        part = wave_sum_u32(part);
-        partc = wave_sum_u32(partc);
+        p0 = wave_sum_u32(p0);
+        p1 = wave_sum_u32(p1);
+        p2 = wave_sum_u32(p2);
         if (lane == 0) {
-            wtot[wave] = part;
-            wcold[wave] = partc;
+            wtot[0][wave] = p0;
+            wtot[1][wave] = p1;
+            wtot[2][wave] = p2;
         }
     }
     __syncthreads();
     uint32_t cold_total = 0;
     {
-        uint32_t carry = 0, carryc = 0;
+        uint32_t tiny_total = 0;
         for (int w = 0; w < RB_WAVES; ++w) {
-            cold_total += wcold[w];
-            if (w < wave) {
-                carry += wtot[w];
-                carryc += wcold[w];
-            }
+            tiny_total += wtot[0][w];
+            cold_total += wtot[0][w] + wtot[1][w];
         }
-        carry += cold_total;
+        const uint32_t lim = (uint32_t)min((int64_t)cold_total, stage_cap);
         bool overflow = false;
-        for (int64_t c = c_lo; c < c_hi; c += 64) {
-            const int64_t s = c + lane;
-            uint32_t keep = 0, total = 0;
-            bool cold = false;
-            if (s < c_hi) {
-                total = cnt[s];
-                keep = keep_of(total);
-                cold = is_cold(total);
+#pragma unroll 1
+        for (int k = 0; k < 3; ++k) {  // one tier at a time: one scan's registers live
+            uint32_t carry = k == 0 ? 0u : k == 1 ? tiny_total : cold_total;
+            for (int w = 0; w < wave; ++w) carry += wtot[k][w];
+            for (int64_t c = c_lo; c < c_hi; c += 64) {
+                const int64_t s = c + lane;
+                uint32_t keep = 0, total = 0;
+                bool mine = false;
+                if (s < c_hi) {
+                    total = cnt[s];
+                    keep = keep_of(total);
+                    mine = tier_of(total) == k;
+                }
+                const uint32_t padded = mine ? (keep + 3u) & ~3u : 0u;
+                const uint32_t incl = wave_incl_scan_u32(padded);
+                if (mine) {
+                    const uint32_t st = carry + incl - padded;
+                    const bool ovf = keep != total;
+                    overflow |= ovf;
+                    const uint32_t flag = ovf || force_stable ? RB_OVF : 0u;
+                    start[s] = st | flag;
+                    cur[s] = flag ? RB_OVF : st;  // pass 2's write cursor (absolute in the stream)
+                    const int64_t g = t * nslots + s;
+                    seg_off[g] = base + st;
+                    // a bucket this kernel reduces itself (after pass 2): a negative length
+                    const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
+                    seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
+                    counts[g] = (int32_t)total;
+                }
+                carry += __builtin_amdgcn_readlane(incl, 63);
             }
-            const bool ovf = keep != total;
-            overflow |= ovf;
-            const uint32_t padded = (keep + 3u) & ~3u;
-            const uint32_t incl = wave_incl_scan_u32(cold ? 0u : padded);
-            const uint32_t inclc = wave_incl_scan_u32(cold ? padded : 0u);
-            const uint32_t st = cold ? carryc + inclc - padded : carry + incl - padded;
-            if (s < c_hi) {
-                const uint32_t flag = ovf || force_stable ? RB_OVF : 0u;
-                start[s] = st | flag;
-                cur[s] = flag ? RB_OVF : st;  // pass 2's write cursor (absolute in the stream)
-                const int64_t g = t * nslots + s;
-                seg_off[g] = base + st;
-                seg_len[g] = (int32_t)keep;
-                counts[g] = (int32_t)total;
-            }
-            carry += __builtin_amdgcn_readlane(incl, 63);
-            carryc += __builtin_amdgcn_readlane(inclc, 63);
         }
         if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
     }
@@ -306,6 +316,22 @@ void records_bucket_kernel(
         const u32x4* sv = (const u32x4*)stage;
         u32x4* ov = (u32x4*)out;  // out = stream base: 16-byte aligned
         for (uint32_t i = threadIdx.x; i < stage_lim / 4; i += blockDim.x) ov[i] = sv[i];
+        // records_stats: the statistics of the staged buckets of <= RB_TINY records, one lane
+        // per bucket straight from LDS (lane_stats: computeStats bit for bit, as the ragged
+        // lane<8> class does), instead of a later kernel re-reading them through a class list
+        if (tiny.num) {
+            for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
+                const uint32_t total = cnt[s];
+                const uint32_t keep = keep_of(total);
+                const uint32_t st = start[s];
+                if (tier_of(total) == 0 && keep >= 1 && st + ((keep + 3u) & ~3u) <= stage_lim) {
+                    const u32x4 a = sv[st / 4];
+                    const u32x4 b = keep > 4 ? sv[st / 4 + 1] : u32x4{~0u, ~0u, ~0u, ~0u};
+                    unsigned v[RB_TINY] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+                    lane_stats<RB_TINY>(v, (int)keep, t * nslots + s, tiny, ColRef{});
+                }
+            }
+        }
     }
     if (!any_ovf) return;
     __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
@@ -360,7 +386,8 @@ template <int W, int REGS>
 static hipError_t launch_bucket(int64_t nstreams, size_t lds_launch, hipStream_t st, const nvrx_record* recs,
                                 const int64_t* rec_off, int64_t nslots, int64_t cap, int force_stable,
                                 int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
-                                int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max) {
+                                int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max,
+                                const nvrx_stats_soa& tiny) {
     static bool attr_set = false;  // per instantiation
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel<W, REGS>,
@@ -370,15 +397,21 @@ static hipError_t launch_bucket(int64_t nstreams, size_t lds_launch, hipStream_t
     }
     hipLaunchKernelGGL((records_bucket_kernel<W, REGS>), dim3((unsigned)nstreams), dim3(64 * W), lds_launch,
                        st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts,
-                       stash_pairs, interleave, stage_cap, cold_max);
+                       stash_pairs, interleave, stage_cap, cold_max, tiny);
     return hipGetLastError();
 }
 
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
-                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st) {
+                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
+                          const nvrx_stats_soa* tiny) {
     if (nstreams <= 0 || nslots <= 0) return hipSuccess;
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
+    static const bool use_tiny = [] {  // NVRX_RB_TINY=0: leave the short buckets to the classes
+        const char* e = getenv("NVRX_RB_TINY");
+        return !(e && atoi(e) == 0);
+    }();
+    const nvrx_stats_soa tiny_soa = (tiny && use_tiny) ? *tiny : nvrx_stats_soa{};
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
     // Streams resident at once = blocks per CU x CUs.  One block per CU (LDS padding) keeps
     // the resident streams and their bucket outputs (scattered 4-B writes) inside the 256 MB
@@ -439,7 +472,7 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
 #define NVRX_RB_LAUNCH(W, REGS)                                                                      \
     return launch_bucket<W, REGS>(nstreams, lds_launch, st, recs, rec_off, nslots, cap, force_stable, \
                                   seg_off, seg_len, out_ns, counts, stash_pairs, stash_interleave, \
-                                  stage_cap, cold_max)
+                                  stage_cap, cold_max, tiny_soa)
     if (waves == 16) {
         if (regs) NVRX_RB_LAUNCH(16, RB_REGS_PER_BLOCK / (64 * 16));
         NVRX_RB_LAUNCH(16, 0);
@@ -463,7 +496,7 @@ hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                          const nvrx_stats_soa& out, uint32_t* col_ref, hipStream_t st) {
     hipError_t e = records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off, seg_len, out_ns,
-                                  counts, st);
+                                  counts, st, &out);
     if (e != hipSuccess) return e;
     const int64_t keep = std::max<int64_t>(1, (cap > 0 && max_len > cap) ? cap : max_len);
     e = segment_stats_ragged(out_ns, seg_off, seg_len, nstreams * nslots, keep, 0, mode, true, out,
