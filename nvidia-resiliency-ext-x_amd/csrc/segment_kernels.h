@@ -2,6 +2,8 @@
 // (segment_stats.hip: strided / one-shot; segment_ragged.hip: length classes).
 // See segment_stats.hip for the algorithm.
 #pragma once
+#include <stdlib.h>
+
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
@@ -65,6 +67,61 @@ struct ColRef {
         if (minbits) atomicOr(&missing[col(s)], 1u);
     }
 };
+
+// ---------------------------------------------------------------------------
+// Length classes of ragged segments (segment_ragged.hip).  Class lists: cls[2c] = first list entry of class c, cls[2c+1] = its
+// count.
+// ---------------------------------------------------------------------------
+namespace ragged {
+enum : int {
+    C_T8 = 0, C_T16, C_T32, C_T64, C_T128,    // lane classes
+    C_W4, C_W8, C_W16, C_W32, C_W64, C_W128,  // wave classes (PL)
+    C_X,                                      // workgroup (EXACT kernel)
+    NCLASS
+};
+
+// need = retained samples + misalignment slack a wave would have to hold
+__device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
+    if (n <= 8) return C_T8;
+    if (n <= 16) return C_T16;
+    if (n <= 32) return C_T32;
+    if (n <= 64) return C_T64;
+    if (n <= 128) return C_T128;
+    if (exact) return C_X;
+    const int need = aligned16 ? n : n + 3;
+    if (need <= 64 * 4) return C_W4;
+    if (need <= 64 * 8) return C_W8;
+    if (need <= 64 * 16) return C_W16;
+    if (need <= 64 * 32) return C_W32;
+    if (need <= 64 * 64) return C_W64;
+    if (need <= 64 * 128) return C_W128;
+    return C_X;
+}
+// Wave-aggregated class counting: one LDS atomic per distinct class present in the
+// wave (leader = lowest lane); returns this lane's rank among same-class lanes plus the
+// class's previous count.  cls < 0: lane does not take part.
+__device__ __forceinline__ uint32_t wave_class_add(uint32_t* lcnt, int cls) {
+    uint64_t pending = __ballot(cls >= 0);
+    uint32_t mine = 0;
+    while (pending) {
+        const int leader = __builtin_ffsll(pending) - 1;
+        const int c = __builtin_amdgcn_readlane(cls, leader);
+        const uint64_t grp = __ballot(cls == c) & pending;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(&lcnt[c], (uint32_t)__popcll(grp));
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (cls == c) mine = base + mbcnt(grp);
+        pending &= ~grp;
+    }
+    return mine;
+}
+}  // namespace ragged
+
+// The class kernels over class-ordered segment lists (segment_ragged.hip): keep = the
+// longest retained segment; classes it rules out are not launched.
+hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                                 int64_t keep, bool aligned16, bool exact, const nvrx_stats_soa& out,
+                                 const ColRef& cr, hipStream_t st);
 
 __device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) {
     // KernelStats() default: num_calls 0, every float NaN (CuptiProfiler.h:39-45)
@@ -246,12 +303,19 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
     const auto real = [&](int i) {
         return !PADSKIP || (unsigned)(eb + 256 * (i >> 2) + (i & 3)) < (unsigned)n;
     };
+    // level-0 bins kept in registers for short segments (see lean_body; PL = 16 would spill
+    // the list kernel's prefetch registers)
+    constexpr bool KEEPBIN = PL <= 8;
+    unsigned hb[KEEPBIN ? PL : 1];
 #pragma unroll
     for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = (lane == 0 && j == 0) ? pad_bin0 : 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < PL; ++i)
-        if (real(i)) atomicAdd(&hist[v[i] >> shift], 1u);
+    for (int i = 0; i < PL; ++i) {
+        const unsigned h = v[i] >> shift;
+        if (KEEPBIN) hb[KEEPBIN ? i : 0] = h;
+        if (real(i)) atomicAdd(&hist[h], 1u);
+    }
     __builtin_amdgcn_wave_barrier();
 
     // ---- median: radix select on d = x - MIN ----
@@ -306,13 +370,23 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
             unsigned base = 0;
             const unsigned lo0 = wlo + (b0 << shift);
             const unsigned width = 1u << shift;
+            if (KEEPBIN && level == 0) {
 #pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const unsigned d = v[i];
-                const bool in = d - lo0 < width;
-                const uint64_t bm = __ballot(in);
-                if (in) hist[base + mbcnt(bm)] = d;
-                base += (unsigned)__popcll(bm);
+                for (int i = 0; i < PL; ++i) {
+                    const bool in = hb[KEEPBIN ? i : 0] == b0;
+                    const uint64_t bm = __ballot(in);
+                    if (in) hist[base + mbcnt(bm)] = v[i];
+                    base += (unsigned)__popcll(bm);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < PL; ++i) {
+                    const unsigned d = v[i];
+                    const bool in = d - lo0 < width;
+                    const uint64_t bm = __ballot(in);
+                    if (in) hist[base + mbcnt(bm)] = d;
+                    base += (unsigned)__popcll(bm);
+                }
             }
             __builtin_amdgcn_wave_barrier();
             const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
@@ -358,7 +432,7 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
 //     puts every sample below hi above every sample at or above it, so the wave max of
 //     d - hi is the largest sample below hi (likewise the min of d - lo), for any range.
 // The wave reductions finish with row_bcast (wave_*_b).
-template <int PL>
+template <int PL, bool KB = true>
 __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
                                           unsigned* hist, const nvrx_stats_soa& out,
                                           const ColRef& cr) {
@@ -424,13 +498,22 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
     const double sq = wave_sum_f64_b(acc);
 
     // ---- first histogram level ----
+    // KEEPBIN (short segments, registers to spare): every sample's level-0 bin stays in a
+    // register, so the level-0 candidate test is one compare instead of a subtract, a shift
+    // and a compare
+    constexpr bool KEEPBIN = KB && PL <= 16;
+    unsigned hb[KEEPBIN ? PL : 1];
     const int bits = 32 - __clz((int)range);
     int shift = bits > LOGNB ? bits - LOGNB : 0;
 #pragma unroll
     for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < PL; ++i) atomicAdd(&hist[v[i] >> shift], 1u);
+    for (int i = 0; i < PL; ++i) {
+        const unsigned h = v[i] >> shift;
+        if (KEEPBIN) hb[KEEPBIN ? i : 0] = h;
+        atomicAdd(&hist[h], 1u);
+    }
     __builtin_amdgcn_wave_barrier();
 
     const unsigned t0 = (unsigned)((n & 1) ? n / 2 : n / 2 - 1);
@@ -482,12 +565,22 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
             unsigned base = 0;
             const unsigned lo0 = wlo + (b0 << shift);
             const unsigned width = 1u << shift;
+            if (KEEPBIN && level == 0) {
 #pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const bool in = v[i] - lo0 < width;
-                const uint64_t bm = __ballot(in);
-                if (in) hist[base + mbcnt(bm)] = v[i];
-                base += (unsigned)__popcll(bm);
+                for (int i = 0; i < PL; ++i) {
+                    const bool in = hb[KEEPBIN ? i : 0] == b0;
+                    const uint64_t bm = __ballot(in);
+                    if (in) hist[base + mbcnt(bm)] = v[i];
+                    base += (unsigned)__popcll(bm);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < PL; ++i) {
+                    const bool in = v[i] - lo0 < width;
+                    const uint64_t bm = __ballot(in);
+                    if (in) hist[base + mbcnt(bm)] = v[i];
+                    base += (unsigned)__popcll(bm);
+                }
             }
             __builtin_amdgcn_wave_barrier();
             const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
@@ -606,7 +699,7 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
 }
 
 // FULL segments only (64*PL samples each, 16-B aligned): lean_body.
-template <int PL, class Segs>
+template <int PL, class Segs, bool KB = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
 void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
     constexpr int NB = Bins<PL>::NB;
@@ -622,60 +715,114 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     int m0;
     unsigned x0;
     load_segment<PL, true>(p, n, v, m0, x0);
-    lean_body<PL>(v, n, x0, s, hist, out, cr);
+    lean_body<PL, KB>(v, n, x0, s, hist, out, cr);
 }
 
-// Ascending bitonic sorting network over N registers (N a power of two): compile-time
-// compare-exchanges, i.e. v_min/v_max pairs -- no LDS, no branches.
+// Batcher's odd-even merge sort over N registers (N a power of two) as a compile-time list of
+// compare-exchanges -- v_min/v_max pairs, no LDS, no branches: 19 / 63 / 191 / 543 / 1471 of them
+// for N = 8 / 16 / 32 / 64 / 128, against the bitonic network's 24 / 80 / 240 / 672 / 1792.
 template <int N>
-__device__ __forceinline__ void sort_net(unsigned (&v)[N]) {
-#pragma unroll
-    for (int k = 2; k <= N; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-#pragma unroll
-            for (int i = 0; i < N; ++i) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const unsigned a = v[i], b = v[l];
-                    const bool up = (i & k) == 0;
-                    v[i] = up ? min(a, b) : max(a, b);
-                    v[l] = up ? max(a, b) : min(a, b);
-                }
-            }
-        }
+struct OemNet {
+    template <class F>
+    static constexpr void walk(F&& f) {
+        for (int p = 1; p < N; p += p)
+            for (int k = p; k > 0; k /= 2)
+                for (int j = k % p; j + k < N; j += k + k)
+                    for (int i = 0; i < k && i + j + k < N; ++i)
+                        if ((i + j) / (p + p) == (i + j + k) / (p + p)) f(i + j, i + j + k);
+    }
+    static constexpr int count() {
+        int c = 0;
+        walk([&](int, int) { ++c; });
+        return c;
+    }
+    static constexpr int NC = count();
+    short a[NC], b[NC];
+    constexpr OemNet() : a(), b() {
+        int c = 0;
+        walk([&](int x, int y) {
+            a[c] = (short)x;
+            b[c] = (short)y;
+            ++c;
+        });
+    }
+};
+// compare-exchanges [LO, HI) of the network, split in halves down to single ones, so every
+// register index is a constant expression (a loop over the table left 128-register networks
+// with runtime indices: the array went to scratch)
+template <int N, int LO, int HI>
+__device__ __forceinline__ void net_range(unsigned (&v)[N]) {
+    if constexpr (HI - LO == 1) {
+        constexpr OemNet<N> net{};
+        constexpr int a = net.a[LO], b = net.b[LO];
+        const unsigned x = v[a], y = v[b];
+        v[a] = min(x, y);
+        v[b] = max(x, y);
+    } else if constexpr (HI - LO > 1) {
+        net_range<N, LO, (LO + HI) / 2>(v);
+        net_range<N, (LO + HI) / 2, HI>(v);
     }
 }
-
-// One segment of 1..N samples per LANE (v: the n samples in any order, slots >= n
-// ignored).  u32 -> f32 us is monotone, so sorting the integer ns sorts the floats
-// computeStats sorts; then CuptiProfiler.cpp:53-71 statement by statement (sequential f32
-// sums over the sorted samples) -- every field bit-exact.
 template <int N>
+__device__ __forceinline__ void sort_net(unsigned (&v)[N]) {
+    net_range<N, 0, OemNet<N>::NC>(v);
+}
+
+constexpr int pow2_ceil(int m) {
+    int p = 1;
+    while (p < m) p += p;
+    return p;
+}
+// v[idx] for a runtime idx known to lie in the compile-time range [LO, HI] (any register of the
+// range otherwise): a multiplexer tree on the bits of idx - LO, one v_cndmask per candidate,
+// instead of a compare and a select per register.
+template <int LO, int HI, int N>
+__device__ __forceinline__ unsigned pick(const unsigned (&v)[N], int idx) {
+    constexpr int P = pow2_ceil(HI - LO + 1);
+    unsigned t[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) t[j] = v[LO + j <= HI ? LO + j : HI];
+    const unsigned k = (unsigned)(idx - LO);
+#pragma unroll
+    for (int w = P, bit = 1; w > 1; w >>= 1, bit += bit) {
+        const bool hi = (k & (unsigned)bit) != 0u;
+#pragma unroll
+        for (int j = 0; j < w / 2; ++j) t[j] = hi ? t[2 * j + 1] : t[2 * j];
+    }
+    return t[0];
+}
+
+// One segment of n samples per LANE, NMIN <= n <= N (v: the n samples in slots [0, n) in any
+// order, slots >= n ignored; a length class guarantees NMIN, so slots below it need no masks).
+// u32 -> f32 us is monotone, so sorting the integer ns sorts the floats computeStats sorts; then
+// CuptiProfiler.cpp:53-71 statement by statement (sequential f32 sums over the sorted samples)
+// -- every field bit-exact.
+template <int N, int NMIN = 1>
 __device__ __forceinline__ void lane_stats(unsigned (&v)[N], int n, int64_t s,
                                            const nvrx_stats_soa& out, const ColRef& cr) {
+    static_assert(NMIN >= 1 && NMIN <= N, "NMIN in [1, N]");
 #pragma unroll
-    for (int j = 0; j < N; ++j) v[j] = j < n ? v[j] : 0xFFFFFFFFu;  // sentinels sort last
+    for (int j = NMIN; j < N; ++j) v[j] = j < n ? v[j] : 0xFFFFFFFFu;  // sentinels sort last
     sort_net<N>(v);
-    const int i0 = (n & 1) ? n / 2 : n / 2 - 1, i1 = n / 2;
-    float fmin = 0.0f, fmax = 0.0f, f0 = 0.0f, f1 = 0.0f, acc = 0.0f;
+    float acc = 0.0f;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const float f = ns_to_us(v[j]);
         v[j] = __float_as_uint(f);
-        if (j == 0) fmin = f;
-        if (j == n - 1) fmax = f;
-        if (j == i0) f0 = f;
-        if (j == i1) f1 = f;
-        acc = j < n ? acc + f : acc;  // accumulate(sorted, 0.0f): sequential f32
+        acc = (j < NMIN || j < n) ? acc + f : acc;  // accumulate(sorted, 0.0f): sequential f32
     }
-    const float med = (n & 1) ? f0 : (f0 + f1) / 2;
+    // s[n-1], s[n/2] and s[n/2 - 1] (the latter read only for even n >= 2)
+    const float fmin = __uint_as_float(v[0]);
+    const float fmax = __uint_as_float(pick<NMIN - 1, N - 1>(v, n - 1));
+    const float f1 = __uint_as_float(pick<NMIN / 2, N / 2>(v, n / 2));
+    const float f0 = __uint_as_float(pick<(NMIN / 2 > 0 ? NMIN / 2 - 1 : 0), N / 2 - 1>(v, n / 2 - 1));
+    const float med = (n & 1) ? f1 : (f0 + f1) / 2;
     const float avg = acc / (float)n;
     float sq = 0.0f;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
         const float t = __uint_as_float(v[j]) - avg;
-        sq = j < n ? sq + t * t : sq;
+        sq = (j < NMIN || j < n) ? sq + t * t : sq;
     }
     out.num[s] = n;
     out.min[s] = fmin;
@@ -788,8 +935,19 @@ template <int PL, class Segs>
 static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
                       const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
-    if (full)  // lean_body: bit-identical to fast_body<PL, true>, 6-9 % faster (tools/mb_c3.hip)
-        hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    static const bool keepbin = [] {  // NVRX_LEAN_KEEPBIN=0: level-0 bins recomputed (A/B)
+        const char* e = getenv("NVRX_LEAN_KEEPBIN");
+        return !(e && atoi(e) == 0);
+    }();
+    // lean_body: bit-identical to fast_body<PL, true>, 6-9 % faster (tools/mb_c3.hip)
+    if constexpr (PL <= 16) {
+        if (full && !keepbin) {
+            hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs, false>), grid, block, 0, st, segs, nseg, out, cr);
+            return;
+        }
+    }
+    if (full)
+        hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs, true>), grid, block, 0, st, segs, nseg, out, cr);
     else
         hipLaunchKernelGGL((seg_stats_fast_kernel<PL, false, Segs>), grid, block, 0, st, segs, nseg, out, cr);
 }

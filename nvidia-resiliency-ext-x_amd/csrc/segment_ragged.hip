@@ -8,7 +8,7 @@
 // classes and each class runs the kernel shaped for it:
 //
 //   n == 0            classifier writes the empty KernelStats (num 0, NaN) itself
-//   n <= 8/32/64/128  one LANE per segment: the samples in registers, a bitonic
+//   n <= 8..128       one LANE per segment: the samples in registers, a sorting
 //                     sorting network, then CuptiProfiler.cpp:53-71 statement by
 //                     statement (sequential f32 sums) -- every field bit-exact
 //   n <= 64*PL        one WAVE per segment (fast_body, segment_kernels.h), PL 4..128
@@ -18,11 +18,108 @@
 // scan, scatter) into one id list ordered by class; every class kernel is persistent
 // (grid = CUs x occupancy) and reads its [start, count) from device memory, so the
 // host never waits for the class sizes.
+#include <stdlib.h>
+
 #include "segment_ragged_kernels.h"
+
+#ifndef NVRX_RAGGED_STREAMS_DEFAULT
+#define NVRX_RAGGED_STREAMS_DEFAULT 2
+#endif
 
 namespace nvrx {
 
 using namespace ragged;
+
+// Side streams of the class kernels: NVRX_RAGGED_STREAMS (1 = everything on the caller's
+// stream), per device, created once.  s[0] is unused: slot 0 is the caller's stream.
+struct Fork {
+    int n;
+    hipStream_t s[4];
+    hipEvent_t fork, join[4];
+};
+static int ragged_streams() {
+    static const int n = [] {
+        const char* e = getenv("NVRX_RAGGED_STREAMS");
+        const int v = e ? atoi(e) : NVRX_RAGGED_STREAMS_DEFAULT;
+        return v < 1 ? 1 : v > 4 ? 4 : v;
+    }();
+    return n;
+}
+static hipError_t ragged_fork(hipStream_t st, Fork*& out) {
+    out = nullptr;
+    const int n = ragged_streams();
+    if (n <= 1) return hipSuccess;
+    static std::mutex mu;
+    static Fork* forks[64] = {nullptr};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipSuccess;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!forks[dev]) {
+            Fork* f = new Fork{};
+            f->n = n;
+            hipError_t e = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming);
+            for (int i = 1; i < n && e == hipSuccess; ++i) {
+                e = hipStreamCreateWithFlags(&f->s[i], hipStreamNonBlocking);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[i], hipEventDisableTiming);
+            }
+            if (e != hipSuccess) return e;  // leaked on failure: a one-time setup
+            forks[dev] = f;
+        }
+    }
+    Fork* f = forks[dev];
+    if (hipError_t e = hipEventRecord(f->fork, st); e != hipSuccess) return e;
+    for (int i = 1; i < f->n; ++i)
+        if (hipError_t e = hipStreamWaitEvent(f->s[i], f->fork, 0); e != hipSuccess) return e;
+    out = f;
+    return hipSuccess;
+}
+static hipError_t ragged_join(hipStream_t st, Fork* f) {
+    for (int i = 1; i < f->n; ++i) {
+        if (hipError_t e = hipEventRecord(f->join[i], f->s[i]); e != hipSuccess) return e;
+        if (hipError_t e = hipStreamWaitEvent(st, f->join[i], 0); e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_list, const uint32_t* cls,
+                                 int64_t keep, bool aligned16, bool exact, const nvrx_stats_soa& out,
+                                 const ColRef& cr, hipStream_t st) {
+    const uint32_t* list = cls_list;
+    const int64_t need = aligned16 ? keep : keep + 3;
+    // class kernels; classes that max_len rules out are not launched.  With side streams the
+    // classes are dealt round robin over them (fork / join by events, which HIP graph capture
+    // follows), so one class's tail and latency-bound waves overlap the next class.
+    Fork* fk = nullptr;
+    if (hipError_t e = ragged_fork(st, fk); e != hipSuccess) return e;
+    int k = 0;
+    const auto S = [&]() {
+        const int i = fk ? k++ % fk->n : 0;
+        return i ? fk->s[i] : st;
+    };
+    const uint32_t* c = cls;
+    ragged_launch_lane(8, segs, list, c + 2 * C_T8, aligned16, out, cr, S());
+    if (keep > 8) ragged_launch_lane(16, segs, list, c + 2 * C_T16, aligned16, out, cr, S());
+    if (keep > 16) ragged_launch_lane(32, segs, list, c + 2 * C_T32, aligned16, out, cr, S());
+    if (keep > 32) ragged_launch_lane(64, segs, list, c + 2 * C_T64, aligned16, out, cr, S());
+    if (keep > 64) ragged_launch_lane(128, segs, list, c + 2 * C_T128, aligned16, out, cr, S());
+    if (!exact) {
+        if (keep > 128) ragged_launch_list(4, segs, list, c + 2 * C_W4, out, cr, S());
+        if (need > 64 * 4) ragged_launch_list(8, segs, list, c + 2 * C_W8, out, cr, S());
+        if (need > 64 * 8) ragged_launch_list(16, segs, list, c + 2 * C_W16, out, cr, S());
+        if (need > 64 * 16) ragged_launch_list(32, segs, list, c + 2 * C_W32, out, cr, S());
+        if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, cr, S());
+        if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, cr, S());
+    }
+    if (exact ? keep > 128 : need > 64 * 128) {
+        if (hipError_t e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, cr, S()); e != hipSuccess)
+            return e;
+    }
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (fk) return ragged_join(st, fk);
+    return hipSuccess;
+}
 
 hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
                                 int64_t nseg, int64_t max_len, int64_t cap, int mode,
@@ -34,7 +131,6 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     RaggedSegs segs{ns, seg_off, seg_len, cap};
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
     if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
-    const int64_t need = aligned16 ? keep : keep + 3;
     const bool exact = mode == NVRX_STATS_EXACT;
     if (nseg >= ((int64_t)1 << 32) - ((int64_t)1 << 26)) return hipErrorInvalidValue;  // 32-bit lists
 
@@ -54,25 +150,9 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
                        cls);
     hipLaunchKernelGGL(classify_scatter_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st,
                        segs, nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, list);
-    // class kernels; classes that max_len rules out are not launched
-    const uint32_t* c = cls;
-    ragged_launch_lane(8, segs, list, c + 2 * C_T8, aligned16, out, cr, st);
-    if (keep > 8) ragged_launch_lane(32, segs, list, c + 2 * C_T32, aligned16, out, cr, st);
-    if (keep > 32) ragged_launch_lane(64, segs, list, c + 2 * C_T64, aligned16, out, cr, st);
-    if (keep > 64) ragged_launch_lane(128, segs, list, c + 2 * C_T128, aligned16, out, cr, st);
-    if (!exact) {
-        if (keep > 128) ragged_launch_list(4, segs, list, c + 2 * C_W4, out, cr, st);
-        if (need > 64 * 4) ragged_launch_list(8, segs, list, c + 2 * C_W8, out, cr, st);
-        if (need > 64 * 8) ragged_launch_list(16, segs, list, c + 2 * C_W16, out, cr, st);
-        if (need > 64 * 16) ragged_launch_list(32, segs, list, c + 2 * C_W32, out, cr, st);
-        if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, cr, st);
-        if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, cr, st);
-    }
-    if (exact ? keep > 128 : need > 64 * 128) {
-        if (hipError_t e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, cr, st); e != hipSuccess)
-            return e;
-    }
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    if (hipError_t e = ragged_launch_classes(segs, list, cls, keep, aligned16, exact, out, cr, st);
+        e != hipSuccess)
+        return e;
     return hipFreeAsync(ws, st);
 }
 

@@ -13,54 +13,12 @@ namespace ragged {
 namespace {  // internal linkage: every translation unit keeps its own copy
 
 
-enum : int {
-    C_T8 = 0, C_T32, C_T64, C_T128,           // lane classes
-    C_W4, C_W8, C_W16, C_W32, C_W64, C_W128,  // wave classes (PL)
-    C_X,                                      // workgroup (EXACT kernel)
-    NCLASS
-};
 constexpr int CLS_THREADS = 1024;
 constexpr int CLS_MAX_BLOCKS = 1024;
 // segment lengths loaded per thread before any is classified: a block's chunk is tens of
 // thousands of segments, and one dependent load per 1024 of them left both passes
 // latency-bound (configs[3]: 153 + 118 us for 33.5 M segments)
 constexpr int CLS_BATCH = 8;
-
-// need = retained samples + misalignment slack a wave would have to hold
-__device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
-    if (n <= 8) return C_T8;
-    if (n <= 32) return C_T32;
-    if (n <= 64) return C_T64;
-    if (n <= 128) return C_T128;
-    if (exact) return C_X;
-    const int need = aligned16 ? n : n + 3;
-    if (need <= 64 * 4) return C_W4;
-    if (need <= 64 * 8) return C_W8;
-    if (need <= 64 * 16) return C_W16;
-    if (need <= 64 * 32) return C_W32;
-    if (need <= 64 * 64) return C_W64;
-    if (need <= 64 * 128) return C_W128;
-    return C_X;
-}
-
-// Wave-aggregated class counting: one LDS atomic per distinct class present in the
-// wave (leader = lowest lane); returns this lane's rank among same-class lanes plus the
-// class's previous count.  cls < 0: lane does not take part.
-__device__ __forceinline__ uint32_t wave_class_add(uint32_t* lcnt, int cls) {
-    uint64_t pending = __ballot(cls >= 0);
-    uint32_t mine = 0;
-    while (pending) {
-        const int leader = __builtin_ffsll(pending) - 1;
-        const int c = __builtin_amdgcn_readlane(cls, leader);
-        const uint64_t grp = __ballot(cls == c) & pending;
-        uint32_t base = 0;
-        if (lane_id() == leader) base = atomicAdd(&lcnt[c], (uint32_t)__popcll(grp));
-        base = __builtin_amdgcn_readlane(base, leader);
-        if (cls == c) mine = base + mbcnt(grp);
-        pending &= ~grp;
-    }
-    return mine;
-}
 
 // pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
 __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
@@ -168,11 +126,17 @@ struct LaneOcc {
     static constexpr int W = N >= 128 ? 2 : N >= 64 ? 4 : N >= 32 ? 6 : 8;
 };
 
+// The shortest segment of a lane class (seg_class): n <= 8, then (N/2, N].
+template <int N>
+struct LaneMin {
+    static constexpr int n = N >= 16 ? N / 2 + 1 : 1;
+};
+
 // Segments per lane per step: each takes a chain of three dependent loads (list entry,
 // descriptor, samples), so the shortest class runs B chains side by side.
 template <int N>
 struct LaneBatch {
-    static constexpr int B = N <= 8 ? 4 : 1;  // 2 for N = 32: 189 -> 214 us (configs[3])
+    static constexpr int B = N <= 8 ? 4 : N <= 16 ? 2 : 1;  // 2 for N = 32: 189 -> 214 us (configs[3])
 };
 
 // One lane per segment of 1..N samples.  u32 -> f32 us is monotone, so sorting the
@@ -219,7 +183,7 @@ void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
         }
 #pragma unroll
         for (int b = 0; b < B; ++b)
-            if (s[b] >= 0) lane_stats<N>(v[b], n[b], s[b], out, cr);
+            if (s[b] >= 0) lane_stats<N, LaneMin<N>::n>(v[b], n[b], s[b], out, cr);
     }
 }
 
