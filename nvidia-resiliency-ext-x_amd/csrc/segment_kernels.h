@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t wave_class_add(uint32_t* lcnt, int cls) {
 // longest retained segment; classes it rules out are not launched.
 hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
                                  int64_t keep, bool aligned16, bool exact, const nvrx_stats_soa& out,
-                                 const ColRef& cr, hipStream_t st);
+                                 hipStream_t st);
 
 __device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) {
     // KernelStats() default: num_calls 0, every float NaN (CuptiProfiler.h:39-45)

@@ -45,17 +45,22 @@ static int ragged_streams() {
     }();
     return n;
 }
+// One caller at a time per process from fork to join (the caller holds `fork_mutex()`): the
+// fork / join events and side streams are shared, and another thread's event record between
+// this caller's record and wait would hand it the wrong dependency.
+static std::mutex& fork_mutex() {
+    static std::mutex mu;
+    return mu;
+}
 static hipError_t ragged_fork(hipStream_t st, Fork*& out) {
     out = nullptr;
     const int n = ragged_streams();
     if (n <= 1) return hipSuccess;
-    static std::mutex mu;
     static Fork* forks[64] = {nullptr};
     int dev = 0;
     if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipSuccess;
     {
-        std::lock_guard<std::mutex> g(mu);
         if (!forks[dev]) {
             Fork* f = new Fork{};
             f->n = n;
@@ -85,12 +90,14 @@ static hipError_t ragged_join(hipStream_t st, Fork* f) {
 
 hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_list, const uint32_t* cls,
                                  int64_t keep, bool aligned16, bool exact, const nvrx_stats_soa& out,
-                                 const ColRef& cr, hipStream_t st) {
+                                 hipStream_t st) {
     const uint32_t* list = cls_list;
     const int64_t need = aligned16 ? keep : keep + 3;
     // class kernels; classes that max_len rules out are not launched.  With side streams the
     // classes are dealt round robin over them (fork / join by events, which HIP graph capture
     // follows), so one class's tail and latency-bound waves overlap the next class.
+    std::unique_lock<std::mutex> lock(fork_mutex(), std::defer_lock);
+    if (ragged_streams() > 1) lock.lock();
     Fork* fk = nullptr;
     if (hipError_t e = ragged_fork(st, fk); e != hipSuccess) return e;
     int k = 0;
@@ -99,21 +106,21 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
         return i ? fk->s[i] : st;
     };
     const uint32_t* c = cls;
-    ragged_launch_lane(8, segs, list, c + 2 * C_T8, aligned16, out, cr, S());
-    if (keep > 8) ragged_launch_lane(16, segs, list, c + 2 * C_T16, aligned16, out, cr, S());
-    if (keep > 16) ragged_launch_lane(32, segs, list, c + 2 * C_T32, aligned16, out, cr, S());
-    if (keep > 32) ragged_launch_lane(64, segs, list, c + 2 * C_T64, aligned16, out, cr, S());
-    if (keep > 64) ragged_launch_lane(128, segs, list, c + 2 * C_T128, aligned16, out, cr, S());
+    ragged_launch_lane(8, segs, list, c + 2 * C_T8, aligned16, out, S());
+    if (keep > 8) ragged_launch_lane(16, segs, list, c + 2 * C_T16, aligned16, out, S());
+    if (keep > 16) ragged_launch_lane(32, segs, list, c + 2 * C_T32, aligned16, out, S());
+    if (keep > 32) ragged_launch_lane(64, segs, list, c + 2 * C_T64, aligned16, out, S());
+    if (keep > 64) ragged_launch_lane(128, segs, list, c + 2 * C_T128, aligned16, out, S());
     if (!exact) {
-        if (keep > 128) ragged_launch_list(4, segs, list, c + 2 * C_W4, out, cr, S());
-        if (need > 64 * 4) ragged_launch_list(8, segs, list, c + 2 * C_W8, out, cr, S());
-        if (need > 64 * 8) ragged_launch_list(16, segs, list, c + 2 * C_W16, out, cr, S());
-        if (need > 64 * 16) ragged_launch_list(32, segs, list, c + 2 * C_W32, out, cr, S());
-        if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, cr, S());
-        if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, cr, S());
+        if (keep > 128) ragged_launch_list(4, segs, list, c + 2 * C_W4, out, S());
+        if (need > 64 * 4) ragged_launch_list(8, segs, list, c + 2 * C_W8, out, S());
+        if (need > 64 * 8) ragged_launch_list(16, segs, list, c + 2 * C_W16, out, S());
+        if (need > 64 * 16) ragged_launch_list(32, segs, list, c + 2 * C_W32, out, S());
+        if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, S());
+        if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, S());
     }
     if (exact ? keep > 128 : need > 64 * 128) {
-        if (hipError_t e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, cr, S()); e != hipSuccess)
+        if (hipError_t e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, S()); e != hipSuccess)
             return e;
     }
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
@@ -125,9 +132,14 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
                                 int64_t nseg, int64_t max_len, int64_t cap, int mode,
                                 bool aligned16, const nvrx_stats_soa& out, uint32_t* col_ref,
                                 int64_t ncols, hipStream_t st) {
-    ColRef cr;
-    if (hipError_t e = make_colref(col_ref, ncols, st, cr); e != hipSuccess) return e;
-    if (nseg <= 0) return hipSuccess;
+    // the column reference (MIN over rows of MED, missing flags) is a column reduction over the
+    // finished statistics (kernel_ref), not per-segment atomics in the class kernels: the class
+    // kernels then carry no column-reference state (fewer SGPRs, fewer spills)
+    const auto colref = [&]() -> hipError_t {
+        if (!col_ref || ncols <= 0) return hipSuccess;
+        return kernel_ref(out.num, out.med, nseg > 0 ? nseg / ncols : 0, ncols, nullptr, col_ref, st);
+    };
+    if (nseg <= 0) return colref();
     RaggedSegs segs{ns, seg_off, seg_len, cap};
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
     if (keep > NVRX_MAX_SEGMENT) return hipErrorInvalidValue;
@@ -145,15 +157,16 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     uint32_t* cls = bcnt + nblocks * NCLASS;
 
     hipLaunchKernelGGL(classify_count_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st, segs,
-                       nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, out, cr);
+                       nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, out);
     hipLaunchKernelGGL(classify_scan_kernel, dim3(1), dim3(CLS_MAX_BLOCKS), 0, st, bcnt, (int)nblocks,
                        cls);
     hipLaunchKernelGGL(classify_scatter_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st,
                        segs, nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, list);
-    if (hipError_t e = ragged_launch_classes(segs, list, cls, keep, aligned16, exact, out, cr, st);
+    if (hipError_t e = ragged_launch_classes(segs, list, cls, keep, aligned16, exact, out, st);
         e != hipSuccess)
         return e;
-    return hipFreeAsync(ws, st);
+    if (hipError_t e = hipFreeAsync(ws, st); e != hipSuccess) return e;
+    return colref();
 }
 
 }  // namespace nvrx

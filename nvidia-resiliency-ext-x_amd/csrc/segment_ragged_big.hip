@@ -6,18 +6,18 @@
 namespace nvrx {
 
 void ragged_launch_list_big(int pl, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                            const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+                            const nvrx_stats_soa& out, hipStream_t st) {
     using namespace ragged;
     if (pl == 64)
-        launch_list<64>(segs, list, cls, out, cr, st);
+        launch_list<64>(segs, list, cls, out, st);
     else
-        launch_list<128>(segs, list, cls, out, cr, st);
+        launch_list<128>(segs, list, cls, out, st);
 }
 
 hipError_t ragged_launch_exact(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                               int64_t max_len, const nvrx_stats_soa& out, const ColRef& cr,
+                               int64_t max_len, const nvrx_stats_soa& out,
                                hipStream_t st) {
-    return ragged::launch_exact_list(segs, list, cls, max_len, out, cr, st);
+    return ragged::launch_exact_list(segs, list, cls, max_len, out, st);
 }
 
 }  // namespace nvrx

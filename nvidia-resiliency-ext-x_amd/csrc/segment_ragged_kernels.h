@@ -23,7 +23,8 @@ constexpr int CLS_BATCH = 8;
 // pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
 __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
     RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, uint32_t* bcnt,
-    nvrx_stats_soa out, ColRef cr) {
+    nvrx_stats_soa out) {
+    const ColRef cr{nullptr, nullptr, 1, 1.0};  // column references: kernel_ref afterwards
     __shared__ uint32_t lcnt[NCLASS];
     if (threadIdx.x < NCLASS) lcnt[threadIdx.x] = 0u;
     __syncthreads();
@@ -144,7 +145,8 @@ struct LaneBatch {
 template <int N>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LaneOcc<N>::W)))
 void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
-                           int aligned16, nvrx_stats_soa out, ColRef cr) {
+                           int aligned16, nvrx_stats_soa out) {
+    const ColRef cr{nullptr, nullptr, 1, 1.0};  // column references: kernel_ref afterwards
     constexpr int B = LaneBatch<N>::B;
     // 32-bit list indices (a 64-bit loop cost lane<8> 315 -> 372 us); the host keeps the
     // segment count below 2^32 - 2^26, so i + B * G never wraps
@@ -207,7 +209,8 @@ constexpr int LIST_CHUNK = 16;
 template <int PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ListOcc<PL>::W)))
 void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
-                           nvrx_stats_soa out, ColRef cr) {
+                           nvrx_stats_soa out) {
+    const ColRef cr{nullptr, nullptr, 1, 1.0};  // column references: kernel_ref afterwards
     constexpr int NB = Bins<PL>::NB;
     __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -275,7 +278,8 @@ template <int NMAX>
 __global__ __launch_bounds__(256) void seg_stats_exact_list_kernel(RaggedSegs segs,
                                                                    const uint32_t* list,
                                                                    const uint32_t* cls,
-                                                                   nvrx_stats_soa out, ColRef cr) {
+                                                                   nvrx_stats_soa out) {
+    const ColRef cr{nullptr, nullptr, 1, 1.0};  // column references: kernel_ref afterwards
     __shared__ __attribute__((aligned(16))) float sbuf[NMAX];
     const uint32_t start = cls[0], cnt = cls[1];
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
@@ -320,33 +324,33 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
 
 template <int N>
 void launch_lane(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls, bool aligned16,
-                 const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+                 const nvrx_stats_soa& out, hipStream_t st) {
     const unsigned blocks = (unsigned)(cu_count() * 2 * LaneOcc<N>::W);
     hipLaunchKernelGGL((seg_stats_lane_kernel<N>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
-                       aligned16 ? 1 : 0, out, cr);
+                       aligned16 ? 1 : 0, out);
 }
 
 template <int PL>
 void launch_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                 const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+                 const nvrx_stats_soa& out, hipStream_t st) {
     const unsigned blocks = (unsigned)(cu_count() * ListOcc<PL>::W);
     hipLaunchKernelGGL((seg_stats_list_kernel<PL>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
-                       out, cr);
+                       out);
 }
 
 hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                             int64_t max_len, const nvrx_stats_soa& out, const ColRef& cr,
+                             int64_t max_len, const nvrx_stats_soa& out,
                              hipStream_t st) {
     const unsigned cus = (unsigned)cu_count();
     if (max_len <= 1024)
         hipLaunchKernelGGL((seg_stats_exact_list_kernel<1024>), dim3(cus * 8), dim3(256), 0, st, segs,
-                           list, cls, out, cr);
+                           list, cls, out);
     else if (max_len <= 8192)
         hipLaunchKernelGGL((seg_stats_exact_list_kernel<8192>), dim3(cus * 4), dim3(256), 0, st, segs,
-                           list, cls, out, cr);
+                           list, cls, out);
     else if (max_len <= NVRX_MAX_SEGMENT)
         hipLaunchKernelGGL((seg_stats_exact_list_kernel<NVRX_MAX_SEGMENT>), dim3(cus), dim3(256), 0,
-                           st, segs, list, cls, out, cr);
+                           st, segs, list, cls, out);
     else
         return hipErrorInvalidValue;
     return hipSuccess;
@@ -358,11 +362,11 @@ hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const
 
 // per-class launches, each defined in the translation unit that instantiates its kernel
 void ragged_launch_lane(int n, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                        bool aligned16, const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st);
+                        bool aligned16, const nvrx_stats_soa& out, hipStream_t st);
 void ragged_launch_list(int pl, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                        const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st);
+                        const nvrx_stats_soa& out, hipStream_t st);
 hipError_t ragged_launch_exact(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                               int64_t max_len, const nvrx_stats_soa& out, const ColRef& cr,
+                               int64_t max_len, const nvrx_stats_soa& out,
                                hipStream_t st);
 
 }  // namespace nvrx

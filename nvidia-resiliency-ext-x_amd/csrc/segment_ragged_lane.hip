@@ -5,17 +5,17 @@
 namespace nvrx {
 
 void ragged_launch_lane128(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                           bool aligned16, const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st);
+                           bool aligned16, const nvrx_stats_soa& out, hipStream_t st);
 
 void ragged_launch_lane(int n, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                        bool aligned16, const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
+                        bool aligned16, const nvrx_stats_soa& out, hipStream_t st) {
     using namespace ragged;
     switch (n) {
-        case 8: launch_lane<8>(segs, list, cls, aligned16, out, cr, st); break;
-        case 16: launch_lane<16>(segs, list, cls, aligned16, out, cr, st); break;
-        case 32: launch_lane<32>(segs, list, cls, aligned16, out, cr, st); break;
-        case 64: launch_lane<64>(segs, list, cls, aligned16, out, cr, st); break;
-        default: ragged_launch_lane128(segs, list, cls, aligned16, out, cr, st); break;
+        case 8: launch_lane<8>(segs, list, cls, aligned16, out, st); break;
+        case 16: launch_lane<16>(segs, list, cls, aligned16, out, st); break;
+        case 32: launch_lane<32>(segs, list, cls, aligned16, out, st); break;
+        case 64: launch_lane<64>(segs, list, cls, aligned16, out, st); break;
+        default: ragged_launch_lane128(segs, list, cls, aligned16, out, st); break;
     }
 }
 

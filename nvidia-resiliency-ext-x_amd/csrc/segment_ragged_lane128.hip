@@ -6,8 +6,8 @@
 namespace nvrx {
 
 void ragged_launch_lane128(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
-                           bool aligned16, const nvrx_stats_soa& out, const ColRef& cr, hipStream_t st) {
-    ragged::launch_lane<128>(segs, list, cls, aligned16, out, cr, st);
+                           bool aligned16, const nvrx_stats_soa& out, hipStream_t st) {
+    ragged::launch_lane<128>(segs, list, cls, aligned16, out, st);
 }
 
 }  // namespace nvrx
