@@ -80,23 +80,21 @@ enum : int {
     NCLASS
 };
 
-// need = retained samples + misalignment slack a wave would have to hold
+// need = retained samples + misalignment slack a wave would have to hold.  Every class is a
+// power-of-two length range, so the class is ceil(log2) of the length, offset: lane classes
+// 1..8 / 9..16 / ... / 65..128, then wave classes of need 129..256 (PL 4) ... 4097..8192 (PL 128).
 __device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
-    if (n <= 8) return C_T8;
-    if (n <= 16) return C_T16;
-    if (n <= 32) return C_T32;
-    if (n <= 64) return C_T64;
-    if (n <= 128) return C_T128;
+    if (n <= 128) {
+        const int l = 32 - __clz(n - 1);  // ceil(log2 n); 0 for n = 1
+        return l <= 3 ? C_T8 : l - 3;     // 4..7 -> C_T16..C_T128
+    }
     if (exact) return C_X;
     const int need = aligned16 ? n : n + 3;
-    if (need <= 64 * 4) return C_W4;
-    if (need <= 64 * 8) return C_W8;
-    if (need <= 64 * 16) return C_W16;
-    if (need <= 64 * 32) return C_W32;
-    if (need <= 64 * 64) return C_W64;
-    if (need <= 64 * 128) return C_W128;
-    return C_X;
+    const int l = 32 - __clz(need - 1);  // 8..13 -> C_W4..C_W128
+    return l <= 13 ? l - 3 : C_X;
 }
+static_assert(C_T16 == 1 && C_T128 == 4 && C_W4 == 5 && C_W128 == 10 && C_X == 11, "class order");
+
 // Wave-aggregated class counting: one LDS atomic per distinct class present in the
 // wave (leader = lowest lane); returns this lane's rank among same-class lanes plus the
 // class's previous count.  cls < 0: lane does not take part.

@@ -156,6 +156,10 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     uint32_t* bcnt = list + nseg;
     uint32_t* cls = bcnt + nblocks * NCLASS;
 
+    // (a one-pass variant -- per-block totals reserving each class's range with global atomics,
+    // lists of nseg entries per class -- measured 4.17 / 4.37 ms with 1024 / 256-thread blocks
+    // against 4.13 for these three launches on configs[3]: the reservations contend on one
+    // address per class)
     hipLaunchKernelGGL(classify_count_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st, segs,
                        nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, out);
     hipLaunchKernelGGL(classify_scan_kernel, dim3(1), dim3(CLS_MAX_BLOCKS), 0, st, bcnt, (int)nblocks,

@@ -20,6 +20,7 @@ constexpr int CLS_MAX_BLOCKS = 1024;
 // latency-bound (configs[3]: 153 + 118 us for 33.5 M segments)
 constexpr int CLS_BATCH = 8;
 
+
 // pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
 __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
     RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, uint32_t* bcnt,
