@@ -152,14 +152,23 @@ __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, i
     const double dn = (double)n;
     const double se = sd - dn * (double)c;  // exact: integers < 2^53
     // lane 0: avg = (n MIN + sd) / (1000 n), rounded once to f32;
-    // lane 1: std = sqrt(n sq - se^2) / (1000 n) as sqrtf of the f32-rounded variance in us^2
-    //         (f64 quotient, then one f32 rounding and a correctly rounded f32 root: ~1e-7
-    //         relative, inside the FAST bar, without the f64 square-root sequence)
+    // lane 1: std = sqrt(n sq - se^2) / (1000 n) as the f32 root of the f32-rounded variance
+    //         in us^2.
+    // The quotient is num times the hardware reciprocal refined by Newton steps (~1e-16
+    // relative, so at most a rounding-boundary case off the correctly rounded f32) and the root
+    // is the hardware v_sqrt_f32 (~1 ulp): both far inside the FAST bars (2.5e-7 / 1e-6
+    // relative), without the f64 divide and correctly rounded sqrt sequences (~20 of ~400 VALU
+    // per segment at 1024 samples).
     const double den = 1000.0 * dn;
     const double vq = __builtin_fma(sq, dn, -(se * se));
     const double num = lane == 0 ? __builtin_fma((double)mn, dn, sd) : (vq > 0.0 ? vq : 0.0);
-    const double q = num / (lane == 0 ? den : den * den);
-    const float r = lane == 0 ? (float)q : __builtin_sqrtf((float)q);
+    const double dd = lane == 0 ? den : den * den;
+    double rc = __builtin_amdgcn_rcp(dd);
+    rc = __builtin_fma(rc, __builtin_fma(-dd, rc, 1.0), rc);
+    rc = __builtin_fma(rc, __builtin_fma(-dd, rc, 1.0), rc);
+    double q = num * rc;
+    q = __builtin_fma(__builtin_fma(-dd, q, num), rc, q);
+    const float r = lane == 0 ? (float)q : __builtin_amdgcn_sqrtf((float)q);
     const float avg = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 0));
     const float sdv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 1));
     if (lane == 0) {
@@ -186,7 +195,9 @@ struct Bins {
 };
 
 // Locate the bucket holding relative rank ta in the wave's histogram (one read of the bins):
-// bucket index, elements in lower buckets, count of the bucket.
+// bucket index, elements in lower buckets, count of the bucket.  Vector work is the row-wise
+// inclusive prefix of the lanes' bin sums (DPP row shifts) and one compare; the row holding ta,
+// the lane inside it (ballot), that lane's bins (readlanes) and the walk over them are scalar.
 template <int PL>
 __device__ __forceinline__ void hist_locate1(const unsigned* hist, unsigned ta, unsigned& ba,
                                              unsigned& bfa, unsigned& ca) {
@@ -199,24 +210,38 @@ __device__ __forceinline__ void hist_locate1(const unsigned* hist, unsigned ta, 
         h[j] = hist[lane * BPL + j];
         local += h[j];
     }
-    const unsigned incl = wave_incl_scan_u32(local);
-    const int La = __popcll(__ballot(incl <= ta));
-    unsigned run = incl - local, sa = 0, pa = 0, na = 0;
-    bool fa = false;
+    unsigned v = local;  // inclusive prefix inside the lane's 16-lane row
+    v += dpp<0x111>(v);
+    v += dpp<0x112>(v);
+    v += dpp<0x114>(v);
+    v += dpp<0x118>(v);
+    const unsigned t0 = rl(v, 15), t1 = t0 + rl(v, 31), t2 = t1 + rl(v, 47);
+    const int row = ta < t0 ? 0 : ta < t1 ? 1 : ta < t2 ? 2 : 3;
+    const unsigned rbase = row == 0 ? 0u : row == 1 ? t0 : row == 2 ? t1 : t2;
+    const uint64_t before = __ballot(v <= ta - rbase) & (0xFFFFull << (16 * row));
+    const int La = min(16 * row + (int)__popcll(before), 63);
+    unsigned hs[BPL], loc = 0;
 #pragma unroll
     for (int j = 0; j < BPL; ++j) {
-        const unsigned nxt = run + h[j];
-        if (!fa && nxt > ta) {
-            fa = true;
-            sa = (unsigned)(lane * BPL + j);
-            pa = run;
-            na = h[j];
+        hs[j] = rl(h[j], La);
+        loc += hs[j];
+    }
+    unsigned run = rbase + rl(v, La) - loc;  // elements below lane La's first bin
+    ba = (unsigned)(La * BPL + BPL - 1);
+    bfa = run;
+    ca = 0;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+        const unsigned nxt = run + hs[j];
+        if (!found && nxt > ta) {
+            found = true;
+            ba = (unsigned)(La * BPL + j);
+            bfa = run;
+            ca = hs[j];
         }
         run = nxt;
     }
-    ba = __builtin_amdgcn_readlane(sa, La);
-    bfa = __builtin_amdgcn_readlane(pa, La);
-    ca = __builtin_amdgcn_readlane(na, La);
 }
 
 // Occupancy target per PL: the samples take PL VGPRs; ask the register allocator for
