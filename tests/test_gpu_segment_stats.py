@@ -303,3 +303,39 @@ def test_ragged_length_classes(mode, aligned16, cap):
     assert np.array_equal(missing, (num.reshape(rows, ncols) == 0).any(axis=0))
     ok = ~missing
     assert np.array_equal(c[:ncols].view(np.float32)[ok], want_ref[ok])
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_FAST, ops.STATS_EXACT])
+@pytest.mark.parametrize("aligned16", [False, True])
+def test_ragged_class_boundaries(mode, aligned16):
+    # every length of the lane classes (1..129: the sorting networks, the class-restricted
+    # masks and the multiplexer selects of s[n-1], s[n/2], s[n/2-1] at both edges of each
+    # class) and the wave-class edges, 6 segments each, with ties and a wide-range segment;
+    # lane classes are bit-exact in every field in both modes
+    rng = np.random.default_rng(20261017)
+    lens = list(range(1, 130)) + [255, 256, 257, 258, 511, 512, 513, 1023, 1024, 1025, 4096, 4097, 8192]
+    lens = np.repeat(np.array(lens, np.int64), 6)
+    if aligned16:
+        lens = (lens + 3) // 4 * 4  # 16-byte aligned starts
+    off = np.zeros(len(lens) + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    host = rng.integers(2000, 2_200_000, size=int(off[-1]), dtype=np.uint32)
+    host[off[6]:off[7]] = 5000  # all ties
+    host[off[-2]:off[-1]:3] = rng.integers(1 << 30, 1 << 32, size=len(host[off[-2]:off[-1]:3]), dtype=np.uint32)
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    st = ops.segment_stats_ragged(ns, torch.from_numpy(off).to(DEV), None, max_len=int(lens.max()),
+                                  cap=8192, mode=mode)
+    g = st.cpu()
+    for s, L in enumerate(lens):
+        r = O.compute_stats(O.ns_to_us(host[off[s]:off[s + 1]]))
+        got = [np.float32(getattr(g, f)[s].item()) for f in ("min", "max", "med", "avg", "std")]
+        want = [np.float32(x) for x in (r.min, r.max, r.median, r.avg, r.stddev)]
+        assert g.num[s].item() == r.num_calls == L, s
+        assert got[:3] == want[:3], (s, L, got, want)
+        if mode == ops.STATS_EXACT or L <= 128:
+            assert got[3:] == want[3:], (s, L, got, want)
+        else:  # FAST: exact mean / std rounded once, or (a segment too long for a misaligned
+            # wave, sent to the workgroup kernel) the reference's own values
+            v = host[off[s]:off[s + 1]].astype(np.float64)
+            assert abs(got[3] - v.mean() / 1000) <= 2.5e-7 * v.mean() / 1000 or got[3] == want[3], (s, L)
+            assert abs(got[4] - v.std() / 1000) <= 1e-6 * v.std() / 1000 + 1e-6 or got[4] == want[4], (s, L)
