@@ -119,13 +119,15 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
         if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, S());
         if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, S());
     }
-    if (exact ? keep > 128 : need > 64 * 128) {
-        if (hipError_t e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, S()); e != hipSuccess)
-            return e;
+    hipError_t e = hipSuccess;
+    if (exact ? keep > 128 : need > 64 * 128) e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, S());
+    if (e == hipSuccess) e = hipGetLastError();
+    // joined on every path: a side stream left forked would leave a graph capture unjoined
+    if (fk) {
+        const hipError_t j = ragged_join(st, fk);
+        if (e == hipSuccess) e = j;
     }
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-    if (fk) return ragged_join(st, fk);
-    return hipSuccess;
+    return e;
 }
 
 hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const int32_t* seg_len,
