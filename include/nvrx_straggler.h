@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NVRX_ABI_VERSION 2
+#define NVRX_ABI_VERSION 3
 
 #define NVRX_OK 0
 #define NVRX_ERR_INVALID -1   /* bad argument / shape */
@@ -233,14 +233,21 @@ int nvrx_profiler_register_kernel(nvrx_profiler* p, const char* name, uint32_t* 
  * host records move to the device log once buffer_size bytes of them wait (and at every
  * get_stats / get_records / reset). */
 int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n);
+/* Slot-numbering generation: bumped by every nvrx_profiler_reset (slots are renumbered from 0
+ * after it).  A caller that builds device records from registered slots reads it after
+ * registering and passes it to nvrx_profiler_ingest. */
+int nvrx_profiler_generation(nvrx_profiler* p, uint64_t* generation);
 /* Append n DEVICE records (push order, after every record staged before) to the device log:
- * one device-to-device copy enqueued on `stream`, so dev_recs must stay valid until that
- * stream reaches it; later profiler calls order themselves after it.  Ignored while stopped.
- * Records whose slot is not registered are not counted.  (While a live capture is started,
- * the copy is itself a kernel dispatch and is recorded like any other.)  No reference
- * counterpart: the device-side entry of an external tracer (SURVEY 8(b)
+ * one copy kernel enqueued on `stream`, so dev_recs must stay valid until that stream reaches
+ * it; later profiler calls order themselves after it.  Ignored while stopped.  `generation`
+ * must be the current nvrx_profiler_generation (NVRX_ERR_STATE otherwise: the slots were
+ * numbered before a reset).  Records whose slot is not registered at this call are dropped
+ * (never counted, even if that slot number is handed out later).  (While a live capture is
+ * started, the copy is itself a kernel dispatch and is recorded like any other.)  No
+ * reference counterpart: the device-side entry of an external tracer (SURVEY 8(b)
  * nvrx_ingest_records). */
-int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n, void* stream);
+int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n,
+                         uint64_t generation, void* stream);
 /* Durations longer than UINT32_MAX ns (4.29 s) are stored saturated at UINT32_MAX; *count =
  * how many since the last reset (the Python layer warns when it is nonzero). */
 int nvrx_profiler_saturated(nvrx_profiler* p, int64_t* count);
@@ -271,6 +278,15 @@ int nvrx_profiler_capture_available(void);
 /* Deliver the dispatch records completed so far to the started / stopped profiler
  * (cuptiActivityFlushAll(0), CuptiProfiler.cpp:138).  Synchronous; no-op without capture. */
 int nvrx_capture_flush(void);
+/* Cost accounting of the live capture since configuration (process-wide, monotone): buffer
+ * callbacks delivered by rocprofiler-sdk, record headers in them, dispatch records handed to a
+ * profiler, wall time spent inside this library's buffer callback, and the number and wall time
+ * of rocprofiler_flush_buffer calls (report-time flushes).  No reference counterpart (CUPTI's
+ * cost is not exposed either); tools/capture_cost.py reads it.  All zero without capture. */
+typedef struct nvrx_capture_counters {
+    int64_t callbacks, headers, dispatches, callback_ns, flushes, flush_ns;
+} nvrx_capture_counters;
+int nvrx_capture_stats(nvrx_capture_counters* out);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -240,7 +240,8 @@ struct nvrx_profiler {
     std::unordered_map<nvrx::DispatchKey, uint32_t, nvrx::DispatchKeyHash> key_to_slot;
     std::vector<nvrx_record> staged;  // host records not yet in the device log
     uint64_t saturated = 0;           // durations clamped to UINT32_MAX ns since the last reset
-    uint64_t version = 0;             // bumped whenever the record set changes
+    uint64_t version = 0;             // bumped whenever the record set or the slot table changes
+    uint64_t generation = 1;          // slot numbering epoch: bumped by every reset
     hipStream_t stream = nullptr;
     hipEvent_t ingest_ev = nullptr;   // last nvrx_profiler_ingest copy (on the caller's stream)
     bool ingest_pending = false;
@@ -595,13 +596,23 @@ int nvrx_profiler_reset(nvrx_profiler* p) {
     p->key_to_slot.clear();
     p->saturated = 0;
     ++p->version;
+    ++p->generation;  // slots handed out before this reset are void
+    return NVRX_OK;
+}
+
+int nvrx_profiler_generation(nvrx_profiler* p, uint64_t* generation) {
+    NVRX_CHECK_ARG(p && generation, "nvrx_profiler_generation: null argument");
+    std::lock_guard<std::mutex> lk(p->mu);
+    *generation = p->generation;
     return NVRX_OK;
 }
 
 int nvrx_profiler_register_kernel(nvrx_profiler* p, const char* name, uint32_t* slot) {
     NVRX_CHECK_ARG(p && name && slot, "nvrx_profiler_register_kernel: null argument");
     std::lock_guard<std::mutex> lk(p->mu);
+    const size_t before = p->names.size();
     *slot = slot_of_name(p, name);
+    if (p->names.size() != before) ++p->version;  // a cached get_stats result is stale
     return NVRX_OK;
 }
 
@@ -618,17 +629,22 @@ int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n) {
     return NVRX_OK;
 }
 
-int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n, void* stream) {
+int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n,
+                         uint64_t generation, void* stream) {
     NVRX_CHECK_ARG(p && n >= 0 && (n == 0 || dev_recs), "nvrx_profiler_ingest: bad arguments");
     std::lock_guard<std::mutex> lk(p->mu);
+    if (generation != p->generation)
+        return fail(NVRX_ERR_STATE, "nvrx_profiler_ingest: slots of another generation (a reset "
+                                    "renumbered them; register the kernels again)");
     if (!p->started || n == 0) return NVRX_OK;  // activity disabled: records are not captured
     DeviceGuard g(p->cfg.device);
     int rc = flush_locked(p);  // host records staged earlier come first (push order)
     if (rc) return rc;
     rc = grow_log(p, p->log_n + n);
     if (rc) return rc;
-    hipError_t e = hipMemcpyAsync(p->d_log + p->log_n, dev_recs, (size_t)n * sizeof(nvrx_record),
-                                  hipMemcpyDeviceToDevice, S(stream));
+    // a copy that drops (slot := UINT32_MAX) records of slots not registered at this call
+    hipError_t e = nvrx::records_ingest(p->d_log + p->log_n, dev_recs, n, (uint32_t)p->names.size(),
+                                        S(stream));
     if (e == hipSuccess) e = hipEventRecord(p->ingest_ev, S(stream));
     if (e != hipSuccess) return hip_status(e, "nvrx_profiler_ingest");
     p->ingest_pending = true;

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,11 +45,9 @@ struct Capture {
     std::atomic<bool> requested{false};  // nvrx_capture_configure succeeded
     std::atomic<nvrx_profiler*> target{nullptr};
     std::atomic<int> inflight{0};        // buffer callbacks running (destroy waits for 0)
-    std::atomic<uint64_t> n_cb{0}, n_rec{0}, n_pushed{0};  // NVRX_CAPTURE_DEBUG=1 counters
-    bool debug = false;
-    // diagnostics of the capture's cost (tools/live_gpt2.py):
-    bool discard = false;       // NVRX_CAPTURE_DISCARD=1: drop records (the tracer alone)
-    bool keep_started = false;  // NVRX_CAPTURE_KEEP_STARTED=1: never stop the dispatch context
+    // cost accounting (nvrx_capture_stats): callbacks, headers, dispatch records handed to the
+    // profiler, time inside our callback, flushes and time inside rocprofiler_flush_buffer
+    std::atomic<uint64_t> n_cb{0}, n_rec{0}, n_pushed{0}, cb_ns{0}, n_flush{0}, flush_ns{0};
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -93,8 +92,9 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
     // in-flight count first, then the target: capture_detach clears the target and then
     // waits for the count to drain, so a callback never touches a destroyed handle
     c.inflight.fetch_add(1);
+    const auto t0 = std::chrono::steady_clock::now();
     nvrx_profiler* p = c.target.load();
-    if (p && !c.discard) {
+    if (p) {
         thread_local std::vector<nvrx::DispatchRec> batch;
         batch.clear();
         for (size_t i = 0; i < num_headers; ++i) {
@@ -117,17 +117,13 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
         c.n_pushed.fetch_add(batch.size());
         if (!batch.empty()) nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
     }
+    c.cb_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now() - t0).count());
     c.inflight.fetch_sub(1);
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
     Capture& c = cap();
-    const char* d = std::getenv("NVRX_CAPTURE_DISCARD");
-    c.discard = d && d[0] == '1';
-    const char* dbg = std::getenv("NVRX_CAPTURE_DEBUG");
-    c.debug = dbg && dbg[0] == '1';
-    const char* k = std::getenv("NVRX_CAPTURE_KEEP_STARTED");
-    c.keep_started = k && k[0] == '1';
     if (rocprofiler_create_context(&c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
     if (rocprofiler_configure_callback_tracing_service(c.sym_ctx,
                                                        ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT,
@@ -183,7 +179,7 @@ int capture_start(nvrx_profiler* p) {
 
 int capture_stop(nvrx_profiler* p) {
     Capture& c = cap();
-    if (!c.ready || c.keep_started) return 0;
+    if (!c.ready) return 0;
     // no flush here: records of kernels enqueued while started are delivered later (buffer
     // watermark, get_stats / reset flush) and still counted, as CUPTI's are
     (void)p;
@@ -193,7 +189,12 @@ int capture_stop(nvrx_profiler* p) {
 int capture_flush() {
     Capture& c = cap();
     if (!c.ready) return 0;
-    return rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool ok = rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS;
+    c.n_flush.fetch_add(1);
+    c.flush_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                             std::chrono::steady_clock::now() - t0).count());
+    return ok ? 0 : -1;
 }
 
 void capture_detach(nvrx_profiler* p) {
@@ -204,10 +205,6 @@ void capture_detach(nvrx_profiler* p) {
     if (c.target.compare_exchange_strong(cur, nullptr) && c.ready)
         (void)rocprofiler_stop_context(c.disp_ctx);
     while (c.inflight.load() != 0) std::this_thread::yield();  // callbacks that loaded p
-    if (c.debug)
-        std::fprintf(stderr, "nvrx capture: %llu callbacks, %llu headers, %llu dispatch records\n",
-                     (unsigned long long)c.n_cb.load(), (unsigned long long)c.n_rec.load(),
-                     (unsigned long long)c.n_pushed.load());
 }
 
 }  // namespace nvrx
@@ -229,6 +226,21 @@ int nvrx_capture_configure(void) {
 }
 
 int nvrx_profiler_capture_available(void) { return cap().ready.load() ? 1 : 0; }
+
+int nvrx_capture_stats(nvrx_capture_counters* out) {
+    if (!out) {
+        nvrx::set_error("nvrx_capture_stats: NULL output");
+        return NVRX_ERR_INVALID;
+    }
+    Capture& c = cap();
+    out->callbacks = (int64_t)c.n_cb.load();
+    out->headers = (int64_t)c.n_rec.load();
+    out->dispatches = (int64_t)c.n_pushed.load();
+    out->callback_ns = (int64_t)c.cb_ns.load();
+    out->flushes = (int64_t)c.n_flush.load();
+    out->flush_ns = (int64_t)c.flush_ns.load();
+    return NVRX_OK;
+}
 
 int nvrx_capture_flush(void) {
     if (nvrx::capture_flush() != 0) {

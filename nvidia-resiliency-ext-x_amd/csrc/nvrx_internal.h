@@ -43,6 +43,9 @@ hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_
                          int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                          const nvrx_stats_soa& out, uint32_t* col_ref, hipStream_t st);
+// dst[i] = src[i] with every slot >= nslots replaced by UINT32_MAX (never counted)
+hipError_t records_ingest(nvrx_record* dst, const nvrx_record* src, int64_t n, uint32_t nslots,
+                          hipStream_t st);
 hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, const int64_t* dst_off,
                             const uint32_t* ns, int64_t nslots, nvrx_record* out, hipStream_t st);
 

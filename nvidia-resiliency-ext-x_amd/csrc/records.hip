@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * RB_WAVES) __attribute__((amdgpu_waves_per_eu(1
 void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
-    int32_t* counts, int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max,
+    int32_t* counts, int64_t stash_pairs, int64_t stage_cap, uint32_t cold_max,
     nvrx_stats_soa tiny) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
@@ -286,7 +286,7 @@ void records_bucket_kernel(
             place(nvrx_record{reg[u].z, reg[u].w});
         }
     }
-    if (snp > 0 && interleave) {
+    {
         const int64_t iters = (np - held) / (64 * RB_UNROLL);
         const int per_it = iters > 0 ? (int)((snp / 64 + iters - 1) / iters) : 0;
         int64_t i = held + lane;
@@ -307,9 +307,8 @@ void records_bucket_kernel(
             place(nvrx_record{w.z, w.w});
         }
         place_stash(1 << 30);
-    } else {
-        place_stash(1 << 30);
-        for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, place);
+        // a chunk that is not pair-aligned (np = 0): its records one by one
+        if (!wpairs) for_records(rs, lo, hi, lane, false, place);
     }
     if (stage_lim > 0) {  // the assembled head of the bucket array, in 16-byte stores
         __syncthreads();
@@ -379,27 +378,15 @@ constexpr size_t RB_LAUNCH_LDS = 160 * 1024 - 256;
 // 64 KiB per SIMD (half its register file) -- 4 waves x 64 pairs per lane (256 VGPRs),
 // 8 x 32 or 16 x 16 (64 VGPRs)
 constexpr int RB_REGS_PER_BLOCK = 16384;
-constexpr int RB_STAGE_KB_DEFAULT = 96;  // LDS staging of the cold buckets
-constexpr int RB_COLD_DEFAULT = 512;     // largest cold bucket (records)
+constexpr int RB_STAGE_KB = 96;  // LDS staging of the cold buckets
+constexpr int RB_COLD = 512;     // largest cold bucket (records)
 
-template <int W, int REGS>
-static hipError_t launch_bucket(int64_t nstreams, size_t lds_launch, hipStream_t st, const nvrx_record* recs,
-                                const int64_t* rec_off, int64_t nslots, int64_t cap, int force_stable,
-                                int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
-                                int64_t stash_pairs, int interleave, int64_t stage_cap, uint32_t cold_max,
-                                const nvrx_stats_soa& tiny) {
-    static bool attr_set = false;  // per instantiation
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel<W, REGS>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
-    hipLaunchKernelGGL((records_bucket_kernel<W, REGS>), dim3((unsigned)nstreams), dim3(64 * W), lds_launch,
-                       st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns, counts,
-                       stash_pairs, interleave, stage_cap, cold_max, tiny);
-    return hipGetLastError();
-}
+// The one shipped configuration: 16 waves x 16 register pairs per lane (4 waves / SIMD, 128
+// VGPRs), LDS stash interleaved with pass 2, 96 KiB of cold-bucket staging, cold = keep <= 512.
+// The alternatives measured on configs[3] (4 / 8 waves, no register pairs, 2-3 blocks per CU,
+// other stage sizes and cold limits, no stash) are in DESIGN.md section 3.4.
+constexpr int RB_WAVES = 16;
+constexpr int RB_REGS = RB_REGS_PER_BLOCK / (64 * RB_WAVES);
 
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
@@ -407,90 +394,42 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
                           const nvrx_stats_soa* tiny) {
     if (nstreams <= 0 || nslots <= 0) return hipSuccess;
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
-    static const bool use_tiny = [] {  // NVRX_RB_TINY=0: leave the short buckets to the classes
-        const char* e = getenv("NVRX_RB_TINY");
-        return !(e && atoi(e) == 0);
-    }();
-    const nvrx_stats_soa tiny_soa = (tiny && use_tiny) ? *tiny : nvrx_stats_soa{};
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
-    // Streams resident at once = blocks per CU x CUs.  One block per CU (LDS padding) keeps
+    const nvrx_stats_soa tiny_soa = tiny ? *tiny : nvrx_stats_soa{};
+    // Streams resident at once = blocks per CU x CUs.  One block per CU (the whole LDS) keeps
     // the resident streams and their bucket outputs (scattered 4-B writes) inside the 256 MB
     // Infinity Cache, where partial lines merge (configs[3]: 5.6 ms with 6 blocks/CU -> 4.4 ms
     // with one, round 1).  That block holds a whole configs[3] stream between the passes:
-    // its LDS stash (~136 KiB) plus RB_REGS_PER_BLOCK register pairs (64 KiB), so pass 2
-    // reads nothing back.  Pass 2 is LDS-atomic latency bound: 16 waves x 16 register pairs
-    // (4 waves per SIMD) beat 8 x 32 and 4 x 64 (configs[3] statistics 5.25 / 5.31 / 5.51 ms,
-    // tools/gpu_ab_waves_regs.sh); without register pairs 16-wave blocks lost to 4 (round 1).
-    // A/B knobs: NVRX_RB_WAVES (4 | 8 | 16), NVRX_RB_BPC (blocks per CU, 0 = as many as fit),
-    // NVRX_RB_REGS=0 (no register pairs), NVRX_RB_STASH (0 = no LDS stash, 1 = not interleaved).
-    static const bool use_regs = [] {
-        const char* e = getenv("NVRX_RB_REGS");
-        return !(e && atoi(e) == 0);
-    }();
-    static const int bpc = [] {
-        const char* e = getenv("NVRX_RB_BPC");
-        return e ? atoi(e) : 1;
-    }();
-    const bool regs = use_regs && bpc == 1;
-    static const int waves_env = [] {
-        const char* e = getenv("NVRX_RB_WAVES");
-        const int w = e ? atoi(e) : 0;
-        return (w == 4 || w == 8 || w == 16) ? w : 0;
-    }();
-    const int waves = waves_env ? waves_env : regs ? 16 : 4;
-    size_t lds_launch = lds;
-    if (bpc > 0) lds_launch = std::max(lds, (size_t)(160 * 1024) / (size_t)bpc - 1024);
-    if (lds_launch > RB_LAUNCH_LDS) lds_launch = std::max(lds, RB_LAUNCH_LDS);
-    // The LDS that the padding leaves over holds the head of every wave's chunk from pass 1
-    // to pass 2 (a whole number of 64-pair wave loads per wave).
-    static const bool use_stash = [] {
-        const char* e = getenv("NVRX_RB_STASH");
-        return !(e && atoi(e) == 0);
-    }();
-    static const int stash_interleave = [] {  // NVRX_RB_STASH=1: stash placed before the rest
-        const char* e = getenv("NVRX_RB_STASH");
-        return (e && atoi(e) == 1) ? 0 : 1;
-    }();
-    // Staging (NVRX_RB_STAGE_KB of LDS, 0 = off; NVRX_RB_COLD = the largest cold bucket)
-    static const int64_t stage_kb = [] {
-        const char* e = getenv("NVRX_RB_STAGE_KB");
-        return (int64_t)(e ? atoi(e) : RB_STAGE_KB_DEFAULT);
-    }();
-    static const uint32_t cold_max = [] {
-        const char* e = getenv("NVRX_RB_COLD");
-        return (uint32_t)(e ? atoi(e) : RB_COLD_DEFAULT);
-    }();
+    // its LDS stash plus RB_REGS_PER_BLOCK register pairs, so pass 2 reads little back.
+    // Pass 2 is LDS-atomic latency bound: 16 waves x 16 register pairs (4 waves per SIMD)
+    // beat 8 x 32 and 4 x 64 (configs[3] statistics 5.25 / 5.31 / 5.51 ms).
+    const size_t lds_launch = std::max(lds, RB_LAUNCH_LDS);
+    // The LDS that the counters leave over: the staged cold buckets, then the head of every
+    // wave's chunk from pass 1 to pass 2 (a whole number of 64-pair wave loads per wave).
     const size_t counters = (size_t)((3 * nslots + 3) & ~(int64_t)3) * sizeof(uint32_t);
     int64_t stage_cap = 0;
     if (lds_launch > counters)
-        stage_cap = std::min<int64_t>(stage_kb * 256, (int64_t)(lds_launch - counters) / 4) & ~(int64_t)3;
+        stage_cap = std::min<int64_t>((int64_t)RB_STAGE_KB * 256, (int64_t)(lds_launch - counters) / 4) & ~(int64_t)3;
     const size_t fixed = counters + (size_t)stage_cap * 4;
     int64_t stash_pairs = 0;
-    if (use_stash && lds_launch > fixed)
-        stash_pairs = (int64_t)((lds_launch - fixed) / (16 * (size_t)waves)) & ~(int64_t)63;
-    if (fixed + (size_t)waves * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
-#define NVRX_RB_LAUNCH(W, REGS)                                                                      \
-    return launch_bucket<W, REGS>(nstreams, lds_launch, st, recs, rec_off, nslots, cap, force_stable, \
-                                  seg_off, seg_len, out_ns, counts, stash_pairs, stash_interleave, \
-                                  stage_cap, cold_max, tiny_soa)
-    if (waves == 16) {
-        if (regs) NVRX_RB_LAUNCH(16, RB_REGS_PER_BLOCK / (64 * 16));
-        NVRX_RB_LAUNCH(16, 0);
+    if (lds_launch > fixed) stash_pairs = (int64_t)((lds_launch - fixed) / (16 * (size_t)RB_WAVES)) & ~(int64_t)63;
+    if (fixed + (size_t)RB_WAVES * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel<RB_WAVES, RB_REGS>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
+        if (e != hipSuccess) return e;
+        attr_set = true;
     }
-    if (waves == 8) {
-        if (regs) NVRX_RB_LAUNCH(8, RB_REGS_PER_BLOCK / (64 * 8));
-        NVRX_RB_LAUNCH(8, 0);
-    }
-    if (regs) NVRX_RB_LAUNCH(4, RB_REGS_PER_BLOCK / (64 * 4));
-    NVRX_RB_LAUNCH(4, 0);
-#undef NVRX_RB_LAUNCH
+    hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)nstreams), dim3(64 * RB_WAVES),
+                       lds_launch, st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns,
+                       counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa);
+    return hipGetLastError();
 }
 
-// Whole record-stream report statistics: bucketing, then length-classed statistics of
-// every bucket; col_ref by a column reduction (cheaper than per-segment atomics once there
-// are many streams).  (Staging the short buckets in LDS and writing them out coalesced,
-// or reducing them inside the bucketing workgroup, were both measured slower on
-// configs[3]: 7.25 / 8.05 ms against 6.9 ms.)
+// Whole record-stream report statistics: bucketing (which reduces the staged buckets of <=
+// RB_TINY records itself), then length-classed statistics of every other bucket; col_ref by a
+// column reduction (cheaper than per-segment atomics once there are many streams).
 hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                          int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
@@ -528,6 +467,24 @@ hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, cons
     if (nslots <= 0) return hipSuccess;
     hipLaunchKernelGGL(records_unbucket_kernel, dim3((unsigned)nslots), dim3(256), 0, st, seg_off,
                        seg_len, dst_off, ns, nslots, out);
+    return hipGetLastError();
+}
+
+// nvrx_profiler_ingest's copy into the device log: slots not registered when the records were
+// handed over are invalidated, so a slot registered later never counts them
+__global__ void records_ingest_kernel(nvrx_record* dst, const nvrx_record* src, int64_t n, uint32_t nslots) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        nvrx_record r = src[i];
+        if (r.slot >= nslots) r.slot = 0xFFFFFFFFu;
+        dst[i] = r;
+    }
+}
+
+hipError_t records_ingest(nvrx_record* dst, const nvrx_record* src, int64_t n, uint32_t nslots,
+                          hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(records_ingest_kernel, dim3((unsigned)blocks), dim3(256), 0, st, dst, src, n, nslots);
     return hipGetLastError();
 }
 

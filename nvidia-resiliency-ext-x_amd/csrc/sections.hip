@@ -10,6 +10,7 @@
 // match to ~1e-16 relative, MIN/MAX/MED exactly).  Sections longer than 16384 timings
 // (CustomSection.max_elapseds_len raised by the user) are sorted the same way in a device
 // scratch buffer by a 1024-thread workgroup.
+#include <algorithm>
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
@@ -122,13 +123,22 @@ hipError_t section_stats(const double* vals, const int64_t* off, int64_t nsec, i
         if (max_len > ((int64_t)1 << 30)) return hipErrorInvalidValue;
         int64_t np2 = 1;
         while (np2 < max_len) np2 <<= 1;
+        // sections are sized by the longest one, so the scratch is bounded by launching a chunk
+        // of sections at a time (at least one): <= 256 MiB unless one section needs more
+        const int64_t per = std::max<int64_t>(1, ((int64_t)256 << 20) / (np2 * (int64_t)sizeof(double)));
+        const int64_t chunk = std::min(nsec, per);
         void* work = nullptr;
-        hipError_t e = hipMallocAsync(&work, (size_t)(nsec * np2) * sizeof(double), st);
+        hipError_t e = hipMallocAsync(&work, (size_t)(chunk * np2) * sizeof(double), st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(section_stats_global_kernel, dim3((unsigned)nsec), dim3(1024), 0, st, vals,
-                           off, (double*)work, np2, num, mn, mx, med, avg, sd);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        return hipFreeAsync(work, st);
+        for (int64_t c0 = 0; c0 < nsec && e == hipSuccess; c0 += chunk) {
+            const int64_t m = std::min(chunk, nsec - c0);
+            hipLaunchKernelGGL(section_stats_global_kernel, dim3((unsigned)m), dim3(1024), 0, st, vals,
+                               off + c0, (double*)work, np2, num + c0, mn + c0, mx + c0, med + c0,
+                               avg + c0, sd + c0);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(work, st);  // on the error path too
+        return e != hipSuccess ? e : f;
     }
     return hipGetLastError();
 }

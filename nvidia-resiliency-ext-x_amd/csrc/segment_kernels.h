@@ -455,7 +455,7 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
 //     puts every sample below hi above every sample at or above it, so the wave max of
 //     d - hi is the largest sample below hi (likewise the min of d - lo), for any range.
 // The wave reductions finish with row_bcast (wave_*_b).
-template <int PL, bool KB = true>
+template <int PL>
 __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
                                           unsigned* hist, const nvrx_stats_soa& out,
                                           const ColRef& cr) {
@@ -524,7 +524,7 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
     // KEEPBIN (short segments, registers to spare): every sample's level-0 bin stays in a
     // register, so the level-0 candidate test is one compare instead of a subtract, a shift
     // and a compare
-    constexpr bool KEEPBIN = KB && PL <= 16;
+    constexpr bool KEEPBIN = PL <= 16;
     unsigned hb[KEEPBIN ? PL : 1];
     const int bits = 32 - __clz((int)range);
     int shift = bits > LOGNB ? bits - LOGNB : 0;
@@ -722,7 +722,7 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
 }
 
 // FULL segments only (64*PL samples each, 16-B aligned): lean_body.
-template <int PL, class Segs, bool KB = true>
+template <int PL, class Segs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
 void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef cr) {
     constexpr int NB = Bins<PL>::NB;
@@ -738,7 +738,7 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     int m0;
     unsigned x0;
     load_segment<PL, true>(p, n, v, m0, x0);
-    lean_body<PL, KB>(v, n, x0, s, hist, out, cr);
+    lean_body<PL>(v, n, x0, s, hist, out, cr);
 }
 
 // Batcher's odd-even merge sort over N registers (N a power of two) as a compile-time list of
@@ -958,19 +958,9 @@ template <int PL, class Segs>
 static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
                       const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
-    static const bool keepbin = [] {  // NVRX_LEAN_KEEPBIN=0: level-0 bins recomputed (A/B)
-        const char* e = getenv("NVRX_LEAN_KEEPBIN");
-        return !(e && atoi(e) == 0);
-    }();
     // lean_body: bit-identical to fast_body<PL, true>, 6-9 % faster (tools/mb_c3.hip)
-    if constexpr (PL <= 16) {
-        if (full && !keepbin) {
-            hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs, false>), grid, block, 0, st, segs, nseg, out, cr);
-            return;
-        }
-    }
     if (full)
-        hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs, true>), grid, block, 0, st, segs, nseg, out, cr);
+        hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else
         hipLaunchKernelGGL((seg_stats_fast_kernel<PL, false, Segs>), grid, block, 0, st, segs, nseg, out, cr);
 }

@@ -18,33 +18,21 @@
 // scan, scatter) into one id list ordered by class; every class kernel is persistent
 // (grid = CUs x occupancy) and reads its [start, count) from device memory, so the
 // host never waits for the class sizes.
-#include <stdlib.h>
+#include <mutex>
 
 #include "segment_ragged_kernels.h"
-
-#ifndef NVRX_RAGGED_STREAMS_DEFAULT
-#define NVRX_RAGGED_STREAMS_DEFAULT 2
-#endif
 
 namespace nvrx {
 
 using namespace ragged;
 
-// Side streams of the class kernels: NVRX_RAGGED_STREAMS (1 = everything on the caller's
-// stream), per device, created once.  s[0] is unused: slot 0 is the caller's stream.
+// The class kernels are dealt over the caller's stream and one side stream per device
+// (configs[3]: 4.28 -> 4.15 ms; 3 / 4 streams were no faster).
+constexpr int RAGGED_STREAMS = 2;
 struct Fork {
-    int n;
-    hipStream_t s[4];
-    hipEvent_t fork, join[4];
+    hipStream_t s[RAGGED_STREAMS];  // s[0] unused: slot 0 is the caller's stream
+    hipEvent_t fork, join[RAGGED_STREAMS];
 };
-static int ragged_streams() {
-    static const int n = [] {
-        const char* e = getenv("NVRX_RAGGED_STREAMS");
-        const int v = e ? atoi(e) : NVRX_RAGGED_STREAMS_DEFAULT;
-        return v < 1 ? 1 : v > 4 ? 4 : v;
-    }();
-    return n;
-}
 // One caller at a time per process from fork to join (the caller holds `fork_mutex()`): the
 // fork / join events and side streams are shared, and another thread's event record between
 // this caller's record and wait would hand it the wrong dependency.
@@ -52,36 +40,53 @@ static std::mutex& fork_mutex() {
     static std::mutex mu;
     return mu;
 }
+// out = nullptr (every class on `st`) unless the side stream of st's device can take work:
+// st must belong to the current device (the side stream is created there) and the side
+// stream must not be inside a graph capture -- once forked into a capture it stays part of
+// it until that capture ends, and another caller's eager work on it would be recorded into
+// that graph.  A capturing `st` forks as usual (the capture follows the events), also into
+// a side stream already joined to that same capture.
 static hipError_t ragged_fork(hipStream_t st, Fork*& out) {
     out = nullptr;
-    const int n = ragged_streams();
-    if (n <= 1) return hipSuccess;
     static Fork* forks[64] = {nullptr};
     int dev = 0;
     if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipSuccess;
-    {
-        if (!forks[dev]) {
-            Fork* f = new Fork{};
-            f->n = n;
-            hipError_t e = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming);
-            for (int i = 1; i < n && e == hipSuccess; ++i) {
-                e = hipStreamCreateWithFlags(&f->s[i], hipStreamNonBlocking);
-                if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[i], hipEventDisableTiming);
-            }
-            if (e != hipSuccess) return e;  // leaked on failure: a one-time setup
-            forks[dev] = f;
+    if (st != nullptr) {
+        hipDevice_t sdev = 0;
+        if (hipError_t e = hipStreamGetDevice(st, &sdev); e != hipSuccess) return e;
+        if ((int)sdev != dev) return hipSuccess;
+    }
+    if (!forks[dev]) {
+        Fork* f = new Fork{};
+        hipError_t e = hipEventCreateWithFlags(&f->fork, hipEventDisableTiming);
+        for (int i = 1; i < RAGGED_STREAMS && e == hipSuccess; ++i) {
+            e = hipStreamCreateWithFlags(&f->s[i], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&f->join[i], hipEventDisableTiming);
         }
+        if (e != hipSuccess) return e;  // leaked on failure: a one-time setup
+        forks[dev] = f;
     }
     Fork* f = forks[dev];
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    unsigned long long id_st = 0;
+    if (hipError_t e = hipStreamGetCaptureInfo(st, &cst, &id_st); e != hipSuccess) return e;
+    for (int i = 1; i < RAGGED_STREAMS; ++i) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        unsigned long long id = 0;
+        if (hipError_t e = hipStreamGetCaptureInfo(f->s[i], &cs, &id); e != hipSuccess) return e;
+        // busy in a capture other than st's own
+        if (cs != hipStreamCaptureStatusNone && !(cst == hipStreamCaptureStatusActive && id == id_st))
+            return hipSuccess;
+    }
     if (hipError_t e = hipEventRecord(f->fork, st); e != hipSuccess) return e;
-    for (int i = 1; i < f->n; ++i)
+    for (int i = 1; i < RAGGED_STREAMS; ++i)
         if (hipError_t e = hipStreamWaitEvent(f->s[i], f->fork, 0); e != hipSuccess) return e;
     out = f;
     return hipSuccess;
 }
 static hipError_t ragged_join(hipStream_t st, Fork* f) {
-    for (int i = 1; i < f->n; ++i) {
+    for (int i = 1; i < RAGGED_STREAMS; ++i) {
         if (hipError_t e = hipEventRecord(f->join[i], f->s[i]); e != hipSuccess) return e;
         if (hipError_t e = hipStreamWaitEvent(st, f->join[i], 0); e != hipSuccess) return e;
     }
@@ -96,13 +101,12 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
     // class kernels; classes that max_len rules out are not launched.  With side streams the
     // classes are dealt round robin over them (fork / join by events, which HIP graph capture
     // follows), so one class's tail and latency-bound waves overlap the next class.
-    std::unique_lock<std::mutex> lock(fork_mutex(), std::defer_lock);
-    if (ragged_streams() > 1) lock.lock();
+    std::lock_guard<std::mutex> lock(fork_mutex());
     Fork* fk = nullptr;
     if (hipError_t e = ragged_fork(st, fk); e != hipSuccess) return e;
     int k = 0;
     const auto S = [&]() {
-        const int i = fk ? k++ % fk->n : 0;
+        const int i = fk ? k++ % RAGGED_STREAMS : 0;
         return i ? fk->s[i] : st;
     };
     const uint32_t* c = cls;
@@ -168,10 +172,10 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
                        cls);
     hipLaunchKernelGGL(classify_scatter_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st,
                        segs, nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, list);
-    if (hipError_t e = ragged_launch_classes(segs, list, cls, keep, aligned16, exact, out, st);
-        e != hipSuccess)
-        return e;
-    if (hipError_t e = hipFreeAsync(ws, st); e != hipSuccess) return e;
+    const hipError_t e = ragged_launch_classes(segs, list, cls, keep, aligned16, exact, out, st);
+    const hipError_t f = hipFreeAsync(ws, st);  // on the error path too
+    if (e != hipSuccess) return e;
+    if (f != hipSuccess) return f;
     return colref();
 }
 

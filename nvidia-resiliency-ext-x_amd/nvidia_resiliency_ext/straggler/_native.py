@@ -13,7 +13,7 @@ import threading
 from typing import Optional
 
 LIB_NAME = "libnvrx_hip.so"
-ABI_VERSION = 2  # include/nvrx_straggler.h NVRX_ABI_VERSION
+ABI_VERSION = 3  # include/nvrx_straggler.h NVRX_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 NVRX_OK = 0
@@ -52,6 +52,11 @@ class ScoreArgs(ctypes.Structure):
 
 class Record(ctypes.Structure):
     _fields_ = [("slot", u32), ("ns", u32)]
+
+
+class CaptureCounters(ctypes.Structure):
+    _fields_ = [("callbacks", i64), ("headers", i64), ("dispatches", i64),
+                ("callback_ns", i64), ("flushes", i64), ("flush_ns", i64)]
 
 
 class ProfilerConfig(ctypes.Structure):
@@ -93,13 +98,15 @@ SIGNATURES = {
     "nvrx_profiler_reset": (ctypes.c_int, [P]),
     "nvrx_profiler_register_kernel": (ctypes.c_int, [P, ctypes.c_char_p, ctypes.POINTER(u32)]),
     "nvrx_profiler_push": (ctypes.c_int, [P, P, i64]),
-    "nvrx_profiler_ingest": (ctypes.c_int, [P, P, i64, P]),
+    "nvrx_profiler_ingest": (ctypes.c_int, [P, P, i64, ctypes.c_uint64, P]),
+    "nvrx_profiler_generation": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_uint64)]),
     "nvrx_profiler_saturated": (ctypes.c_int, [P, ctypes.POINTER(i64)]),
     "nvrx_profiler_get_stats": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P, P, P, P, P, P, P]),
     "nvrx_profiler_kernel_name": (ctypes.c_int, [P, u32, ctypes.c_char_p, i64]),
     "nvrx_profiler_get_records": (ctypes.c_int, [P, i64, ctypes.POINTER(i64), P]),
     "nvrx_profiler_capture_available": (ctypes.c_int, []),
     "nvrx_capture_flush": (ctypes.c_int, []),
+    "nvrx_capture_stats": (ctypes.c_int, [ctypes.POINTER(CaptureCounters)]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

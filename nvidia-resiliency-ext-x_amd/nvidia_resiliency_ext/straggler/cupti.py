@@ -180,17 +180,28 @@ class KernelProfiler:
         recs[:, 1] = np.minimum(d, 0xFFFFFFFF)
         N.call("nvrx_profiler_push", self._h, recs.ctypes.data, len(slots))
 
-    def ingest(self, records, stream=None) -> None:
+    @property
+    def generation(self) -> int:
+        """Slot-numbering generation (bumped by every reset): pass the value read after
+        registering to ``ingest`` so records built from slots of an earlier interval raise."""
+        g = ctypes.c_uint64()
+        N.call("nvrx_profiler_generation", self._h, ctypes.byref(g))
+        return int(g.value)
+
+    def ingest(self, records, stream=None, generation: Optional[int] = None) -> None:
         """Append DEVICE records: an int32/uint32 tensor [n, 2] of {slot, ns} (registered slots,
         push order) resident on the profiler's device, copied into the device record log on
-        `stream` (default: the current stream) -- no host round trip."""
+        `stream` (default: the current stream) -- no host round trip.  ``generation``: the
+        ``self.generation`` the slots were registered under (default: the current one); a
+        reset since then raises RuntimeError.  Records of unregistered slots are dropped."""
         import torch
 
         N.require_device(records, "records")
         if records.dim() != 2 or records.shape[1] != 2 or records.element_size() != 4:
             raise ValueError("records must be a [n, 2] tensor of 32-bit {slot, ns}")
         records = records.contiguous()
-        N.call("nvrx_profiler_ingest", self._h, records.data_ptr(), records.shape[0],
+        gen = self.generation if generation is None else int(generation)
+        N.call("nvrx_profiler_ingest", self._h, records.data_ptr(), records.shape[0], gen,
                N.stream_handle(stream if stream is not None else torch.cuda.current_stream(records.device)))
 
     def saturated(self) -> int:
@@ -217,6 +228,10 @@ class KernelProfiler:
                                               *(p(c) for c in cols)), "get_stats")
             if int(count.value) <= n:
                 break
+        # the count may also have shrunk (a reset from another thread): only count.value
+        # entries were written
+        m = int(count.value)
+        slots, num, cols = slots[:m], num[:m], [c[:m] for c in cols]
         sat = self.saturated()
         if sat:
             warnings.warn(f"{sat} captured kernel duration(s) above 4.29 s stored saturated at "
@@ -334,7 +349,7 @@ class CuptiManager:
         with self.lock:
             return self.cupti_ext.register_kernel(name)
 
-    def ingest(self, records, stream=None):
+    def ingest(self, records, stream=None, generation=None):
         """Device-resident {slot, ns} records from an external tracer into the active run."""
         with self.lock:
-            self.cupti_ext.ingest(records, stream)
+            self.cupti_ext.ingest(records, stream, generation)

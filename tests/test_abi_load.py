@@ -31,7 +31,7 @@ def test_python_binding_covers_header():
 
 def test_lib_loads_and_reports_abi():
     L = _native.lib()
-    assert L.nvrx_abi_version() == 2
+    assert L.nvrx_abi_version() == _native.ABI_VERSION == 3
     cnt = ctypes.c_int(-1)
     # no HIP device in the CPU container: the call succeeds (0 devices) or reports HIP error
     rc = L.nvrx_device_count(ctypes.byref(cnt))
@@ -53,3 +53,11 @@ def test_synth_header_symbols_exported():
     lib = ctypes.CDLL(os.path.join(os.path.dirname(_native.LIB_PATH), "libnvrx_synth.so"))
     for n in _declared("nvrx_synth.h"):
         assert hasattr(lib, n), n
+
+
+def test_capture_counters_without_capture():
+    # the cost accounting of the live capture: all zero while no tool is configured
+    c = _native.CaptureCounters()
+    assert _native.lib().nvrx_capture_stats(ctypes.byref(c)) == 0
+    assert (c.callbacks, c.dispatches, c.flushes, c.callback_ns) == (0, 0, 0, 0)
+    assert _native.lib().nvrx_capture_stats(None) == _native.NVRX_ERR_INVALID

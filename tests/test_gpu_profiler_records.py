@@ -275,6 +275,36 @@ def test_profiler_ingest_device_records():
         p.close()
 
 
+def test_profiler_ingest_rejects_slots_from_before_a_reset():
+    # slots are renumbered by reset; records built from a slot of the previous
+    # interval must not be counted under whichever kernel took that number afterwards, and a
+    # record of a slot registered only after the ingest call is never counted
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=64)
+    try:
+        p.initialize()
+        p.start()
+        old = p.register_kernel("old_blk_1_1_1_grid_1_1_1")
+        g_old = p.generation
+        rec = lambda s, ns: torch.from_numpy(  # noqa: E731
+            np.array([[s, ns]] * 4, np.uint32).view(np.int32)).cuda()
+        p.reset()
+        assert p.generation == g_old + 1
+        new = p.register_kernel("new_blk_1_1_1_grid_1_1_1")
+        assert new == old == 0  # the same number, another kernel
+        with pytest.raises(RuntimeError, match="generation"):
+            p.ingest(rec(old, 7000), generation=g_old)
+        p.ingest(rec(new, 3000), generation=p.generation)
+        p.ingest(rec(1, 5000))  # slot 1 is not registered yet: dropped
+        later = p.register_kernel("later_blk_1_1_1_grid_1_1_1")
+        assert later == 1
+        st = p.get_stats()
+        assert set(st) == {"new_blk_1_1_1_grid_1_1_1"}
+        assert st["new_blk_1_1_1_grid_1_1_1"].num_calls == 4
+        assert st["new_blk_1_1_1_grid_1_1_1"].median == np.float32(3.0)
+    finally:
+        p.close()
+
+
 def test_profiler_drains_staged_records_at_the_watermark():
     # bufferSize 8 KiB = 1024 records: pushes beyond it go to the device log right away
     # (host memory bounded); the statistics are those of every record

@@ -1,7 +1,7 @@
 """Diagnostics of the live capture on the GPU box: do the dispatch records of many launches all
 arrive?  DIAG_N launches split over DIAG_SECTIONS start/stop sections, a capture flush every
 DIAG_FLUSH_EVERY sections (0: none), DIAG_SYNC_EVERY sections a device synchronize;
-NVRX_CAPTURE_DEBUG=1 prints the capture's counters at destroy."""
+nvrx_capture_stats (CaptureCounters) reports the capture's counters."""
 import os
 import sys
 import time

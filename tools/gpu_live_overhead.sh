@@ -6,5 +6,4 @@ L="python -u tools/live_gpt2.py --steps 40 --base-steps 20"
 MASTER_PORT=29541 timeout -k 10 300 $L --out gpurun_out/live/o_full.json > gpurun_out/live/o_full.log 2>&1
 MASTER_PORT=29542 NVRX_CAPTURE_WATERMARK=6291456 timeout -k 10 300 $L --out gpurun_out/live/o_wm6m.json > gpurun_out/live/o_wm6m.log 2>&1
 MASTER_PORT=29543 NVRX_CAPTURE_WATERMARK=131072 timeout -k 10 300 $L --out gpurun_out/live/o_wm128k.json > gpurun_out/live/o_wm128k.log 2>&1
-MASTER_PORT=29544 NVRX_CAPTURE_DISCARD=1 timeout -k 10 300 $L --out gpurun_out/live/o_discard.json > gpurun_out/live/o_discard.log 2>&1
 echo ok
