@@ -106,8 +106,20 @@ int nvrx_abi_version(void);
 int nvrx_device_count(int* count);             /* synchronous */
 int nvrx_sync(void* stream);                   /* synchronous: waits for `stream` */
 
+/* ---------------------------------------------------------------- durations */
+/* Every duration the library reads is a u32 DURATION KEY.  The reference keeps
+ * (end - start) / 1000.0f (CuptiProfiler.cpp:187): the u64 ns difference rounded to f32, then
+ * divided.  A key is the integer ns below NVRX_KEY_WIDE (3.76 s) and the f32 bits of f32(ns)
+ * above it (0xE0000000 + bits(f32(ns)) - bits(f32(0xE0000000)), at most 0xF0200000), so it
+ * keeps exactly what the reference keeps for any u64 duration, and keys order like the
+ * durations.  nvrx_duration_key encodes one (host); a tracer feeding nvrx_profiler_ingest or a
+ * matrix of durations of 3.76 s and more must encode them.  Below 3.76 s keys are plain ns. */
+#define NVRX_KEY_WIDE 0xE0000000u
+#define NVRX_KEY_WIDE_F32BITS 0x4F600000u /* bits of f32(0xE0000000) */
+uint32_t nvrx_duration_key(uint64_t ns);
+
 /* ---------------------------------------------------------------- statistics */
-/* Segment s = ns[s*seg_stride + seg_begin : + seg_len] (uint32 ns durations); the
+/* Segment s = ns[s*seg_stride + seg_begin : + seg_len] (uint32 duration keys); the
  * last min(seg_len, cap) samples are retained (cap <= 0: all).  out->* are [nseg].
  * col_ref (optional, [2*ncols] uint32): segments form a [nseg/ncols][ncols] rank x kernel
  * matrix; the call also produces the per-kernel relative reference of _all_reduce_times
@@ -168,9 +180,8 @@ int nvrx_section_stats(const double* vals, const int64_t* off, int64_t nsec, int
                        double* sd, void* stream);
 
 /* ---------------------------------------------------------------- record streams */
-/* A record is one kernel execution: the slot of its composite kernel name and its
- * duration in ns (end - start, CuptiProfiler.cpp:187; saturated at UINT32_MAX = 4.29 s,
- * counted by nvrx_profiler_saturated). */
+/* A record is one kernel execution: the slot of its composite kernel name and its duration
+ * key (end - start, CuptiProfiler.cpp:187; nvrx_duration_key above 3.76 s). */
 typedef struct nvrx_record {
     uint32_t slot;
     uint32_t ns;
@@ -248,8 +259,8 @@ int nvrx_profiler_generation(nvrx_profiler* p, uint64_t* generation);
  * nvrx_ingest_records). */
 int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n,
                          uint64_t generation, void* stream);
-/* Durations longer than UINT32_MAX ns (4.29 s) are stored saturated at UINT32_MAX; *count =
- * how many since the last reset (the Python layer warns when it is nonzero). */
+/* *count = captured / pushed durations of 3.76 s or more (stored as wide keys, nothing lost)
+ * since the last reset: a diagnostic of hung or very long kernels. */
 int nvrx_profiler_saturated(nvrx_profiler* p, int64_t* count);
 /* Flush, then compute stats of every slot with >= 1 record.  Synchronous.
  * Returns the number of kernels in *count; fills up to `cap_out` entries of slots

@@ -48,6 +48,14 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 extern "C" {
 
 const char* nvrx_last_error(void) { return g_last_error.c_str(); }
+
+uint32_t nvrx_duration_key(uint64_t ns) {
+    if (ns < NVRX_KEY_WIDE) return (uint32_t)ns;
+    const float f = (float)ns;  // u64 -> f32, round to nearest: CuptiProfiler.cpp:187's conversion
+    uint32_t b;
+    std::memcpy(&b, &f, sizeof b);
+    return NVRX_KEY_WIDE + (b - NVRX_KEY_WIDE_F32BITS);
+}
 int nvrx_abi_version(void) { return NVRX_ABI_VERSION; }
 
 int nvrx_device_count(int* count) {
@@ -239,7 +247,7 @@ struct nvrx_profiler {
     // live-capture fast path: (kernel id, block, grid) -> slot, no string work per record
     std::unordered_map<nvrx::DispatchKey, uint32_t, nvrx::DispatchKeyHash> key_to_slot;
     std::vector<nvrx_record> staged;  // host records not yet in the device log
-    uint64_t saturated = 0;           // durations clamped to UINT32_MAX ns since the last reset
+    uint64_t saturated = 0;           // wide-key durations (>= 3.76 s) since the last reset
     uint64_t version = 0;             // bumped whenever the record set or the slot table changes
     uint64_t generation = 1;          // slot numbering epoch: bumped by every reset
     hipStream_t stream = nullptr;
@@ -467,12 +475,11 @@ void profiler_push_dispatches(nvrx_profiler* p, const DispatchRec* r, size_t n,
                 slot = slot_of_name(p, composite_name(r[i].key));  // CuptiProfiler.cpp:182-185
                 p->key_to_slot.emplace(r[i].key, slot);
             }
-            uint32_t ns = (uint32_t)r[i].ns;
-            if (r[i].ns > 0xFFFFFFFFull) {  // > 4.29 s: saturate, counted
-                ns = 0xFFFFFFFFu;
-                ++p->saturated;
-            }
-            p->staged.push_back(nvrx_record{slot, ns});
+            // CuptiProfiler.cpp:187 keeps f32(end - start): the duration key carries exactly
+            // that for any u64 (the integer ns below 3.76 s)
+            const uint32_t key = nvrx_duration_key(r[i].ns);
+            if (key >= NVRX_KEY_WIDE) ++p->saturated;
+            p->staged.push_back(nvrx_record{slot, key});
         }
         ++p->version;
     }
@@ -623,6 +630,7 @@ int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n) {
     const uint32_t nslots = (uint32_t)p->names.size();
     for (int64_t i = 0; i < n; ++i)
         if (recs[i].slot >= nslots) return fail(NVRX_ERR_INVALID, "nvrx_profiler_push: unknown slot");
+    for (int64_t i = 0; i < n; ++i) p->saturated += recs[i].ns >= NVRX_KEY_WIDE;
     p->staged.insert(p->staged.end(), recs, recs + n);
     ++p->version;
     if ((int64_t)p->staged.size() >= p->drain_records) return flush_locked(p);

@@ -179,14 +179,38 @@ __device__ __forceinline__ void lane_sums_f64(const unsigned (&v)[PL], uint64_t&
     sq = q0 + q1;
 }
 
+// Duration keys.  The reference keeps (end - start) / 1000.0f (CuptiProfiler.cpp:187): the u64
+// ns difference converted to f32, then divided.  Every statistic it reports is therefore a
+// function of f32(ns) alone, so a 32-bit key that is exactly ns below NVRX_KEY_WIDE (3.76 s) and
+// the f32 bits of f32(ns) above it (offset to follow on) loses nothing and keeps the order:
+//   key(ns) = ns                                              ns <  0xE0000000
+//           = 0xE0000000 + bits(f32(ns)) - bits(f32(0xE0000000))   otherwise (<= 0xF0200000 for
+//                                                              ns < 2^64)
+// MIN / MAX / MED select on keys exactly as on ns; the FAST sums use d = key - MIN and are
+// exact below NVRX_KEY_WIDE (segments reaching it take a decoded f64 pass instead).
+#ifndef NVRX_KEY_WIDE  // also in include/nvrx_straggler.h
+#define NVRX_KEY_WIDE 0xE0000000u
+#define NVRX_KEY_WIDE_F32BITS 0x4F600000u  // bits of f32(0xE0000000) = 1.75 * 2^31
+#endif
+
+// f32(ns) of a key: the value the reference divides by 1000
+__host__ __device__ __forceinline__ float key_to_f32(unsigned k) {
+    return k < NVRX_KEY_WIDE ? (float)k : __builtin_bit_cast(float, k - NVRX_KEY_WIDE + NVRX_KEY_WIDE_F32BITS);
+}
+
 // CuptiProfiler.cpp:187 -- (end - start) / 1000.0f: integer ns -> f32 (round to nearest),
 // then the correctly rounded f32 quotient by 1000.  Computed as one f64 multiply by
 // RN(1/1000) rounded to f32 (4 VALU instead of the 11-instruction f32 divide sequence):
 // x = f32(ns) is exact in f64 and the product is within 2^-52 relative of x/1000, while
 // x/1000 is never an f32 rounding midpoint (its odd part would need > 24 bits) and lies at
 // least 2^-24 relative away from every other one, so both round to the same f32.  Checked
-// exhaustively for all 2^32 inputs (tests/test_oracle_golden.py re-checks a sample).
-__device__ __forceinline__ float ns_to_us(unsigned ns) {
+// exhaustively for all 2^32 inputs (tests/test_oracle_golden.py re-checks a sample); the
+// argument depends on the 24-bit significand only, so it holds for the f32 values of wide keys.
+__device__ __forceinline__ float ns_to_us(unsigned key) {
+    return (float)((double)key_to_f32(key) * (1.0 / 1000.0));
+}
+// the same for a key known to lie below NVRX_KEY_WIDE (the key is the ns)
+__device__ __forceinline__ float ns_to_us_narrow(unsigned ns) {
     return (float)((double)(float)ns * (1.0 / 1000.0));
 }
 

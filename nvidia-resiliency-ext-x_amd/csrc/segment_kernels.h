@@ -142,7 +142,7 @@ __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, i
                                            double sd, double sq, unsigned c, const ColRef& cr) {
     const int lane = lane_id();
     const unsigned x = lane == 0 ? mn : lane == 1 ? mx : lane == 2 ? mn + d0 : mn + d1;
-    const float f = ns_to_us(x);
+    const float f = mx < NVRX_KEY_WIDE ? ns_to_us_narrow(x) : ns_to_us(x);  // wave-uniform
     const float fmn = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 0));
     const float fmx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 1));
     const float f0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, f), 2));
@@ -179,6 +179,28 @@ __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, i
         o.avg[s] = avg;
         o.std[s] = sdv;
         cr.add(s, med);
+    }
+}
+
+// FAST AVG / STD of a segment whose keys reach NVRX_KEY_WIDE (a kernel of 3.76 s or more): the
+// integer sums of the bodies do not apply to f32-valued keys, so lane 0 overwrites what
+// emit_stats stored with the mean and population std of the decoded f32(ns) values in f64, each
+// rounded once to f32 us -- two strided passes over the segment p[0:n) in memory (no register
+// arrays: this rare branch must not raise the bodies' register pressure).
+__device__ __forceinline__ void wide_moments(const uint32_t* p, int n, int64_t s, const nvrx_stats_soa& o) {
+    const int lane = lane_id();
+    double a = 0.0;
+    for (int i = lane; i < n; i += 64) a += (double)key_to_f32(p[i]);
+    const double mean = wave_sum_f64(a) / (double)n;
+    double q = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        const double e = (double)key_to_f32(p[i]) - mean;
+        q = __builtin_fma(e, e, q);
+    }
+    const double var = wave_sum_f64(q) / (double)n;
+    if (lane == 0) {
+        o.avg[s] = (float)(mean / 1000.0);
+        o.std[s] = (float)(__builtin_sqrt(var) / 1000.0);
     }
 }
 
@@ -265,7 +287,7 @@ struct OccV {  // the masked PL=128 variant gets the whole 256-register budget
 // FULL: every slot is a sample (m0 = 0, n = 64*PL).  !FULL: slots outside [0, n) were
 // set to x0 (a sample) by the caller.
 template <int PL, bool FULL>
-__device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
+__device__ __forceinline__ unsigned fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
                                           int64_t s, unsigned* hist, const nvrx_stats_soa& out,
                                           const ColRef& cr) {
     constexpr int NB = Bins<PL>::NB;
@@ -440,6 +462,7 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
     }
 
     emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
+    return mx;
 }
 
 // Lean body for FULL segments (n = 64*PL, every slot a sample) -- the C2/C3 matrix path,
@@ -456,7 +479,7 @@ __device__ __forceinline__ void fast_body(unsigned (&v)[PL], int n, int m0, unsi
 //     d - hi is the largest sample below hi (likewise the min of d - lo), for any range.
 // The wave reductions finish with row_bcast (wave_*_b).
 template <int PL>
-__device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
+__device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
                                           unsigned* hist, const nvrx_stats_soa& out,
                                           const ColRef& cr) {
     constexpr int NB = Bins<PL>::NB;
@@ -634,6 +657,7 @@ __device__ __forceinline__ void lean_body(unsigned (&v)[PL], int n, unsigned x0,
         shift = shift > LOGNB ? shift - LOGNB : 0;
     }
     emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
+    return mx;
 }
 
 // HBM -> VGPR in two steps, so a caller can issue the next segment's loads before it
@@ -718,7 +742,8 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     int m0;
     unsigned x0;
     load_segment<PL, FULL>(p, n, v, m0, x0);
-    fast_body<PL, FULL>(v, n, m0, x0, s, hist, out, cr);
+    // returns MAX: keys of >= 3.76 s take the decoded moments (rare, wave-uniform)
+    if (fast_body<PL, FULL>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
 }
 
 // FULL segments only (64*PL samples each, 16-B aligned): lean_body.
@@ -738,7 +763,7 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     int m0;
     unsigned x0;
     load_segment<PL, true>(p, n, v, m0, x0);
-    lean_body<PL>(v, n, x0, s, hist, out, cr);
+    if (lean_body<PL>(v, n, x0, s, hist, out, cr) >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
 }
 
 // Batcher's odd-even merge sort over N registers (N a power of two) as a compile-time list of
@@ -828,9 +853,12 @@ __device__ __forceinline__ void lane_stats(unsigned (&v)[N], int n, int64_t s,
     for (int j = NMIN; j < N; ++j) v[j] = j < n ? v[j] : 0xFFFFFFFFu;  // sentinels sort last
     sort_net<N>(v);
     float acc = 0.0f;
+    // keys of 3.76 s and more (rare) are decoded; the wave takes the plain conversion unless
+    // one of its lanes holds such a key
+    const bool wide = __ballot(pick<NMIN - 1, N - 1>(v, n - 1) >= NVRX_KEY_WIDE) != 0;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-        const float f = ns_to_us(v[j]);
+        const float f = wide ? ns_to_us(v[j]) : ns_to_us_narrow(v[j]);
         v[j] = __float_as_uint(f);
         acc = (j < NMIN || j < n) ? acc + f : acc;  // accumulate(sorted, 0.0f): sequential f32
     }

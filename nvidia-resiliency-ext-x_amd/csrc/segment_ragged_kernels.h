@@ -256,7 +256,8 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
                 int m0;
                 unsigned x0;
                 finish_loads<PL, false>(p, n, v, m0, x0);
-                fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+                if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
+                    wide_moments(p, n, s, out);
 #pragma unroll
                 for (int i = 0; i < PL; ++i) v[i] = w[i];
                 s = s2;
@@ -269,7 +270,8 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
                 int m0;
                 unsigned x0;
                 load_segment<PL, false>(p, n, v, m0, x0);
-                fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr);
+                if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
+                    wide_moments(p, n, s, out);
             }
         }
     }

@@ -71,6 +71,7 @@ SIGNATURES = {
     "nvrx_last_error": (ctypes.c_char_p, []),
     "nvrx_capture_configure": (ctypes.c_int, []),
     "nvrx_abi_version": (ctypes.c_int, []),
+    "nvrx_duration_key": (u32, [ctypes.c_uint64]),
     "nvrx_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "nvrx_sync": (ctypes.c_int, [P]),
     "nvrx_segment_stats_strided": (ctypes.c_int, [P, i64, i64, i64, i64, i64, i32,
@@ -169,6 +170,22 @@ def stream_handle(stream=None) -> Optional[int]:
 
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
+
+
+KEY_WIDE = 0xE0000000
+KEY_WIDE_F32BITS = 0x4F600000
+
+
+def duration_keys(ns):
+    """u64 ns (array-like) -> u32 duration keys (include/nvrx_straggler.h): the ns below
+    0xE0000000 (3.76 s), else 0xE0000000 + bits(f32(ns)) - bits(f32(0xE0000000)) -- exactly
+    the f32(end - start) CuptiProfiler.cpp:187 keeps.  Vectorised twin of nvrx_duration_key."""
+    import numpy as np
+
+    ns = np.asarray(ns, dtype=np.uint64)
+    f = ns.astype(np.float32).view(np.uint32).astype(np.uint64)
+    wide = np.uint64(KEY_WIDE) + f - np.uint64(KEY_WIDE_F32BITS)
+    return np.where(ns < KEY_WIDE, ns, wide).astype(np.uint32)
 
 
 def require_device(t, name: str = "tensor") -> None:

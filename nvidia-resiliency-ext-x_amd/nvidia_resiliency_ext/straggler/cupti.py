@@ -168,16 +168,12 @@ class KernelProfiler:
         self.push_slots(np.full(d.size, self.register_kernel(name), np.uint32), d)
 
     def push_slots(self, slots: np.ndarray, durations_ns: np.ndarray) -> None:
-        """Records of registered slots (valid until the next reset).  Durations above
-        UINT32_MAX ns (4.29 s) are stored saturated, with a warning (the record format keeps
-        integer ns in 32 bits)."""
-        d = np.asarray(durations_ns, dtype=np.uint64)
-        if d.size and int(d.max()) > 0xFFFFFFFF:
-            warnings.warn(f"{int((d > 0xFFFFFFFF).sum())} kernel duration(s) above 4.29 s stored "
-                          "saturated at 4294967295 ns", RuntimeWarning, stacklevel=2)
+        """Records of registered slots (valid until the next reset), durations in ns (any
+        u64): stored as duration keys (_native.duration_keys), which keep exactly the f32(ns)
+        the reference's (end - start) / 1000.0f keeps (CuptiProfiler.cpp:187)."""
         recs = np.empty((len(slots), 2), dtype=np.uint32)
         recs[:, 0] = slots
-        recs[:, 1] = np.minimum(d, 0xFFFFFFFF)
+        recs[:, 1] = N.duration_keys(durations_ns)
         N.call("nvrx_profiler_push", self._h, recs.ctypes.data, len(slots))
 
     @property
@@ -205,7 +201,8 @@ class KernelProfiler:
                N.stream_handle(stream if stream is not None else torch.cuda.current_stream(records.device)))
 
     def saturated(self) -> int:
-        """Durations stored saturated at UINT32_MAX ns since the last reset."""
+        """Durations of 3.76 s or more (wide duration keys; nothing lost) since the last
+        reset -- a count of hung or very long kernels."""
         c = ctypes.c_int64()
         N.call("nvrx_profiler_saturated", self._h, ctypes.byref(c))
         return int(c.value)
@@ -232,10 +229,6 @@ class KernelProfiler:
         # entries were written
         m = int(count.value)
         slots, num, cols = slots[:m], num[:m], [c[:m] for c in cols]
-        sat = self.saturated()
-        if sat:
-            warnings.warn(f"{sat} captured kernel duration(s) above 4.29 s stored saturated at "
-                          "4294967295 ns", RuntimeWarning, stacklevel=2)
         names = [self._name_of(int(s)) for s in slots]
         return KernelSummaries(names, num, *cols)
 

@@ -61,6 +61,16 @@ struct Ring {
     }
 };
 
+// (float)(end - start) of the duration a key encodes (nvrx_oracle.c oracle_duration_key):
+// the integer ns below 3.76 s, the stored f32 value above
+inline float key_to_f32(uint32_t k) {
+    if (k < 0xE0000000u) return (float)(uint64_t)k;
+    const uint32_t b = k - 0xE0000000u + 0x4F600000u;
+    float f;
+    std::memcpy(&f, &b, sizeof f);
+    return f;
+}
+
 }  // namespace
 
 extern "C" void oracle_baseline_matrix_stats(const uint32_t* ns, int64_t nseg, int64_t stride,
@@ -75,10 +85,8 @@ extern "C" void oracle_baseline_matrix_stats(const uint32_t* ns, int64_t nseg, i
             for (int64_t s = lo; s < hi; ++s) {
                 Ring ring((size_t)(cap > 0 ? cap : (len > 0 ? len : 1)));
                 const uint32_t* p = ns + s * stride + begin;
-                for (int64_t i = 0; i < len; ++i) {
-                    const uint64_t start = 0, end = p[i];
-                    ring.push((float)(end - start) / 1000.0f);  // CuptiProfiler.cpp:187
-                }
+                for (int64_t i = 0; i < len; ++i)  // CuptiProfiler.cpp:187 on the key's f32(ns)
+                    ring.push(key_to_f32(p[i]) / 1000.0f);
                 const Stats k = compute_stats(ring.linearize());
                 num[s] = k.num;
                 mn[s] = k.mn;
@@ -111,8 +119,7 @@ extern "C" void oracle_baseline_records_stats(const uint32_t* recs, const int64_
                 for (int64_t i = 0; i < n; ++i) {
                     const uint32_t s = r[2 * i];
                     if (s >= (uint32_t)nslots) continue;
-                    const uint64_t start = 0, end = r[2 * i + 1];
-                    rings[s].push((float)(end - start) / 1000.0f);
+                    rings[s].push(key_to_f32(r[2 * i + 1]) / 1000.0f);  // CuptiProfiler.cpp:187
                 }
                 for (int64_t s = 0; s < nslots; ++s) {
                     const Stats k = compute_stats(rings[s].linearize());

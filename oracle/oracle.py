@@ -72,6 +72,11 @@ def lib():
         L.oracle_baseline_records_stats.argtypes = [P, P, i64, i64, i64, P, P, P, P, P, P,
                                                     ctypes.c_int]
         L.oracle_records_stats.argtypes = [P, P, i64, i64, i64, P, P, P, P, P, P, ctypes.c_int]
+        L.oracle_duration_key.argtypes = [u64]
+        L.oracle_duration_key.restype = ctypes.c_uint32
+        L.oracle_key_to_us.argtypes = [ctypes.c_uint32]
+        L.oracle_key_to_us.restype = ctypes.c_float
+        L.oracle_records_moments.argtypes = [P, P, i64, i64, i64, P, P, ctypes.c_int]
         L.oracle_kernel_ref.argtypes = [P, P, i64, i64, P]
         L.oracle_scores.argtypes = [P, P, P, i64, i64, P, P, P, P, P]
         L.oracle_score_partials.argtypes = [P, P, P, i64, i64, P, P, P, P]
@@ -114,6 +119,31 @@ def ns_to_us(ns) -> np.ndarray:
     ns = np.asarray(ns, dtype=np.uint64)
     f = ns.astype(np.float32)  # RN, exact below 2**24
     return (f / np.float32(1000.0)).astype(np.float32)
+
+
+KEY_WIDE = 0xE0000000
+KEY_WIDE_F32BITS = 0x4F600000
+
+
+def duration_key(ns) -> np.ndarray:
+    """u64 ns -> u32 duration keys (the record-log / matrix element format, nvrx_common.h):
+    ns below 0xE0000000, else 0xE0000000 + bits(f32(ns)) - bits(f32(0xE0000000))."""
+    ns = np.asarray(ns, dtype=np.uint64)
+    f = ns.astype(np.float32).view(np.uint32).astype(np.uint64)
+    wide = np.uint64(KEY_WIDE) + f - np.uint64(KEY_WIDE_F32BITS)
+    return np.where(ns < KEY_WIDE, ns, wide).astype(np.uint32)
+
+
+def key_to_f32(keys) -> np.ndarray:
+    """f32(ns) of duration keys (what the reference divides by 1000)."""
+    k = np.asarray(keys, dtype=np.uint32)
+    wide = (k.astype(np.uint64) - KEY_WIDE + KEY_WIDE_F32BITS).astype(np.uint32).view(np.float32)
+    return np.where(k < KEY_WIDE, k.astype(np.float32), wide).astype(np.float32)
+
+
+def key_to_us(keys) -> np.ndarray:
+    """CuptiProfiler.cpp:187 applied to the durations keys encode: f32(ns) / 1000.0f."""
+    return (key_to_f32(keys) / np.float32(1000.0)).astype(np.float32)
 
 
 def compute_stats(values_f32) -> KStats:
@@ -180,6 +210,20 @@ def records_stats(recs: np.ndarray, rec_off: np.ndarray, nslots: int, cap: int =
 
 
 # ---------------------------------------------------------------- scoring
+def records_moments(recs: np.ndarray, rec_off: np.ndarray, nslots: int, cap: int = 0,
+                    nthreads: int = 1):
+    """Exact mean and population std (us, float64) of every retained (stream, slot) run: what
+    the FAST-mode AVG / STD are checked against (2.5e-7 / 1e-6 relative)."""
+    recs = np.ascontiguousarray(recs, dtype=np.uint32)
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.int64)
+    nstreams = rec_off.size - 1
+    mean = np.empty(nstreams * nslots, np.float64)
+    std = np.empty(nstreams * nslots, np.float64)
+    lib().oracle_records_moments(_p(recs), _p(rec_off), nstreams, nslots, cap, _p(mean), _p(std),
+                                 nthreads)
+    return mean, std
+
+
 def kernel_ref(num: np.ndarray, med: np.ndarray) -> np.ndarray:
     R, K = num.shape
     ref = np.empty(K, np.float32)

@@ -25,6 +25,7 @@ import pytest
 import torch
 
 import oracle as O
+from _fastbars import check_avg_std
 from nvidia_resiliency_ext.straggler import batch, synth
 
 pytestmark = pytest.mark.gpu
@@ -151,12 +152,14 @@ def test_config3_full_world():
         g = _stats_host(rep)
         h = recs.cpu().numpy().view(np.uint32)
         ref = O.records_stats(h, h_off, K, cap=cap, nthreads=THREADS)
+        # AVG / STD of EVERY bucket: bit-exact for <= 16 records, else within the FAST bars of
+        # the exact moments (segments of > 128 samples included)
+        xm, xs = O.records_moments(h, h_off, K, cap=cap, nthreads=THREADS)
         del h
         _check_report(f"zipf R={R} report {i + 1}", R, K, g, ref, res, hist)
         assert np.array_equal(res.stragglers_relative, strag.astype(bool))
-        short = ref["num"] <= 128  # lane classes: every field bit-exact
-        for f in ("avg", "std"):
-            assert np.array_equal(g[f][short].view(np.uint32), ref[f][short].view(np.uint32)), f
+        check_avg_std(g["avg"], g["std"], ref, xm, xs, f"zipf report {i + 1}")
+        del xm, xs
     rev = torch.flip(recs.view(R, N, 2), dims=[1]).reshape(R * N, 2)
     del recs
     rep2 = batch.MatrixReporter(R, K, cap=cap, thr_rel=THR, thr_ind=THR)
@@ -164,7 +167,7 @@ def test_config3_full_world():
     b = _stats_host(rep2)
     for f in EXACT_FIELDS:
         assert np.array_equal(g[f].view(np.uint32), b[f].view(np.uint32)), f
-    short = g["num"] <= 128
+    short = g["num"] <= 16
     for f in ("avg", "std"):
         assert np.array_equal(g[f][short].view(np.uint32), b[f][short].view(np.uint32)), f
         np.testing.assert_allclose(b[f], g[f], rtol=2.5e-7, atol=0)

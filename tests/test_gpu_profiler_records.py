@@ -6,6 +6,7 @@ import pytest
 import torch
 
 import oracle as O
+from _fastbars import check_avg_std
 from nvidia_resiliency_ext.straggler import cupti, ops
 
 pytestmark = pytest.mark.gpu
@@ -179,11 +180,18 @@ def test_cupti_manager_refcount():
         m.shutdown()
 
 
+# FAST mode with 0 < cap <= the LDS stage runs records_resident.hip (one pass, buckets never
+# written); cap 0 / EXACT / too many slots for its LDS run records_bucket + the ragged classes.
+# (52, 8192, 900, 1100): ~52k records per stream, past the 48,128 a workgroup holds in VGPRs
+# (its records re-read from memory at every pass); (500, 100, ...): rings overflow in several
+# LDS groups; (6000, 100, ...): the resident kernel's largest slot tables; (9000, 8192, ...): a
+# stage too small for the ring (bucketing path)
 @pytest.mark.parametrize("nslots,cap,lo,hi", [(37, 8192, 0, 40), (37, 5, 0, 30), (3000, 0, 0, 3),
-                                              (500, 100, 0, 150), (64, 8192, 60, 70)])
+                                              (500, 100, 0, 150), (64, 8192, 60, 70),
+                                              (52, 8192, 900, 1100), (6000, 100, 0, 6),
+                                              (9000, 8192, 0, 3)])
 def test_records_stats_fused_matches_oracle(nslots, cap, lo, hi):
-    # short retained runs reduced inside the bucketing workgroup, the rest by the ragged
-    # kernels: every field vs the oracle's ring-push + computeStats restatement
+    # every field vs the oracle's ring-push + computeStats restatement
     rng = np.random.default_rng(nslots + cap + hi)
     nstreams = 6
     recs, off = _streams(rng, nstreams, nslots, lo, hi)
@@ -201,12 +209,10 @@ def test_records_stats_fused_matches_oracle(nslots, cap, lo, hi):
     ref = O.records_stats(recs, off.astype(np.int64), nslots, cap=cap, nthreads=4)
     for f in ("num", "min", "max", "med"):
         assert np.array_equal(getattr(st, f).numpy().view(np.int32), ref[f].view(np.int32)), f
-    short = (ref["num"] > 0) & (ref["num"] <= 128)
-    for f in ("avg", "std"):
-        a = getattr(st, f).numpy()
-        assert np.array_equal(a[short].view(np.int32), ref[f][short].view(np.int32)), f
-        both = ref["num"] > 0
-        np.testing.assert_allclose(a[both], ref[f][both], rtol=1e-4)
+    # AVG / STD: bit-exact for <= 16 records, else bit-exact or within the FAST bars of the
+    # exact moments (2.5e-7 / 1e-6)
+    xm, xs = O.records_moments(recs, off.astype(np.int64), nslots, cap=cap, nthreads=4)
+    check_avg_std(st.avg.numpy(), st.std.numpy(), ref, xm, xs, f"nslots={nslots} cap={cap}")
     num = ref["num"].reshape(nstreams, nslots)
     want = O.kernel_ref(num, ref["med"].reshape(nstreams, nslots))
     c = col.cpu().numpy()
@@ -327,14 +333,69 @@ def test_profiler_drains_staged_records_at_the_watermark():
         p.close()
 
 
-def test_profiler_saturates_durations_above_uint32_with_a_warning():
-    p = cupti.KernelProfiler(statsMaxLenPerKernel=16)
+@pytest.mark.parametrize("exact", [True, False])
+def test_profiler_durations_of_any_length(exact):
+    # a hung kernel's magnitude must reach MAX / MED.  The reference keeps
+    # (end - start) / 1000.0f (CuptiProfiler.cpp:187) of the u64 difference; duration keys carry
+    # f32(ns) exactly, so 6 s, 5000 s and 2^64-1 ns come out as the reference's floats, bit for
+    # bit (EXACT: every field; FAST: NUM/MIN/MAX/MED, AVG/STD within the FAST bars)
+    ns = np.array([6_000_000_000, 1000, 5_000_000_000_000, 3_758_096_383, 3_758_096_384,
+                   2**64 - 1, 250_000, 4_294_967_296], np.uint64)
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=64, exact=exact)
     try:
         p.initialize()
         p.start()
-        with pytest.warns(RuntimeWarning, match="saturated"):
-            p.push("slow_blk_1_1_1_grid_1_1_1", [5_000_000_000, 1000])
-        s = p.get_stats()["slow_blk_1_1_1_grid_1_1_1"]
-        assert s.max == np.float32(np.float32(4294967295) / np.float32(1000.0))
+        name = "hung_blk_1_1_1_grid_1_1_1"
+        p.push(name, ns)
+        p.push("one_blk_1_1_1_grid_1_1_1", [7_000_000_000])
+        st = p.get_stats()
+        ref = O.compute_stats(O.ns_to_us(ns))  # the reference's floats of the raw u64 ns
+        s = st[name]
+        assert s.num_calls == ns.size
+        assert (np.float32(s.min), np.float32(s.max), np.float32(s.median)) == \
+            (np.float32(ref.min), np.float32(ref.max), np.float32(ref.median))
+        assert np.float32(s.max) == np.float32(np.float32(2.0**64) / np.float32(1000.0))
+        if exact:
+            assert (np.float32(s.avg), np.float32(s.stddev)) == (np.float32(ref.avg), np.float32(ref.stddev))
+        else:
+            v = O.key_to_f32(O.duration_key(ns)).astype(np.float64)
+            np.testing.assert_allclose(s.avg, v.mean() / 1000, rtol=2.5e-7)
+            np.testing.assert_allclose(s.stddev, v.std() / 1000, rtol=1e-6)
+        one = st["one_blk_1_1_1_grid_1_1_1"]
+        assert one.max == one.median == np.float32(np.float32(7e9) / np.float32(1000.0))
+        assert p.saturated() == 6  # durations of >= 3.76 s (wide keys), counted
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("n", [5, 40, 3000])
+def test_records_stats_wide_keys(n):
+    # FAST record statistics (records_resident.hip: lane path <= 16 records, wave path above)
+    # over buckets mixing narrow and wide duration keys: MIN/MAX/MED bit-exact with the
+    # reference's floats, AVG/STD within the FAST bars of the decoded values' moments
+    rng = np.random.default_rng(n)
+    nslots, nstreams = 3, 2
+    d = []
+    for t in range(nstreams):
+        for s in range(nslots):
+            ns = rng.integers(1000, 9_000_000_000 if s != 1 else 5_000_000, size=n, dtype=np.uint64)
+            if s == 2:
+                ns[rng.integers(0, n)] = 2**63 + 12345
+            d.append((s, ns))
+    slots = np.concatenate([np.full(x.size, s, np.uint32) for s, x in d])
+    keys = np.concatenate([O.duration_key(x) for _, x in d])
+    recs = np.ascontiguousarray(np.stack([slots, keys], 1))
+    off = np.arange(nstreams + 1, dtype=np.int64) * (nslots * n)
+    st = ops.records_stats(torch.from_numpy(recs.view(np.int32)).cuda(), torch.from_numpy(off).cuda(),
+                           nslots, 8192, n, mode=ops.STATS_FAST).cpu()
+    for g, (s, ns) in enumerate(d):
+        ref = O.compute_stats(O.ns_to_us(ns))
+        assert st.num[g].item() == n
+        got = [np.float32(getattr(st, f)[g].item()) for f in ("min", "max", "med")]
+        assert got == [np.float32(ref.min), np.float32(ref.max), np.float32(ref.median)], (g, s)
+        if n <= 16:
+            assert np.float32(st.avg[g].item()) == np.float32(ref.avg)
+        else:
+            v = O.key_to_f32(O.duration_key(ns)).astype(np.float64) if s != 1 else ns.astype(np.float64)
+            np.testing.assert_allclose(st.avg[g].item(), v.mean() / 1000, rtol=2.5e-7)
+            np.testing.assert_allclose(st.std[g].item(), v.std() / 1000, rtol=1e-6)

@@ -11,6 +11,7 @@ import pytest
 import torch
 
 import oracle as O
+from _fastbars import key_values
 from nvidia_resiliency_ext.straggler import ops, synth
 
 pytestmark = pytest.mark.gpu
@@ -27,7 +28,7 @@ def _exact_avg_std(host_ns, nseg, stride, begin, length, cap):
     avg = np.empty(nseg)
     std = np.empty(nseg)
     for s in range(nseg):
-        seg = host_ns[s * stride + begin + length - keep: s * stride + begin + length].astype(np.float64)
+        seg = key_values(host_ns[s * stride + begin + length - keep: s * stride + begin + length])
         avg[s] = seg.mean() / 1000.0
         std[s] = seg.std() / 1000.0
     return avg, std
@@ -327,7 +328,7 @@ def test_ragged_class_boundaries(mode, aligned16):
                                   cap=8192, mode=mode)
     g = st.cpu()
     for s, L in enumerate(lens):
-        r = O.compute_stats(O.ns_to_us(host[off[s]:off[s + 1]]))
+        r = O.compute_stats(O.key_to_us(host[off[s]:off[s + 1]]))  # u32 duration keys
         got = [np.float32(getattr(g, f)[s].item()) for f in ("min", "max", "med", "avg", "std")]
         want = [np.float32(x) for x in (r.min, r.max, r.median, r.avg, r.stddev)]
         assert g.num[s].item() == r.num_calls == L, s
@@ -336,6 +337,6 @@ def test_ragged_class_boundaries(mode, aligned16):
             assert got[3:] == want[3:], (s, L, got, want)
         else:  # FAST: exact mean / std rounded once, or (a segment too long for a misaligned
             # wave, sent to the workgroup kernel) the reference's own values
-            v = host[off[s]:off[s + 1]].astype(np.float64)
+            v = key_values(host[off[s]:off[s + 1]])
             assert abs(got[3] - v.mean() / 1000) <= 2.5e-7 * v.mean() / 1000 or got[3] == want[3], (s, L)
             assert abs(got[4] - v.std() / 1000) <= 1e-6 * v.std() / 1000 + 1e-6 or got[4] == want[4], (s, L)
