@@ -190,9 +190,10 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
                bucket_plus_stats_ms=stats_ms,
                hbm_frac_of_report=R * N * RECORD_BYTES / (tmax / steps) / HBM_PEAK,
                hbm_frac_of_stats=R * N * RECORD_BYTES / (stats_ms * 1e-3) / HBM_PEAK,
-               alg_bytes_per_record=RECORD_BYTES,
-               straggler_sets_exact=bool(np.array_equal(
-                   res.stragglers_relative, synth.straggler_ranks(R).astype(bool))))
+               alg_bytes_per_record=RECORD_BYTES, steps=steps,
+               kernels_per_rank=shard_sizes(K, world),
+               straggler_sets_exact=all_ranks(bool(np.array_equal(
+                   res.stragglers_relative, synth.straggler_ranks(R).astype(bool))), world, dev))
     if world == 1 and rank == 0 and cpu_ranks > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
@@ -225,6 +226,20 @@ def cpu_threads() -> int:
 
 def comm_max(x: float, world: int, dev) -> float:
     return allreduce(x, torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
+
+
+def all_ranks(flag: bool, world: int, dev) -> bool:
+    """True iff the flag holds on every rank (MIN over ranks)."""
+    return bool(allreduce(1.0 if flag else 0.0, torch.distributed.ReduceOp.MIN if world > 1 else None,
+                          world, dev) > 0.5)
+
+
+def shard_sizes(K_global: int, world: int):
+    """Kernels per rank under hash(name) % world (synth.shard_kernels), for every rank."""
+    if world == 1:
+        return [K_global]
+    names = synth.kernel_names(K_global)
+    return [int(synth.shard_kernels(names, world, r).size) for r in range(world)]
 
 
 def pmc_traffic(workload: str):
@@ -315,27 +330,33 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3)
     res = r["res"]
     strag_true = synth.straggler_ranks(C2["R"])
-    sets_ok = bool(np.array_equal(res.stragglers_relative, strag_true.astype(bool)))
+    sets_ok = all_ranks(bool(np.array_equal(res.stragglers_relative, strag_true.astype(bool))),
+                        world, dev)
+    # what the process group itself reports (not the launcher's --gpus)
+    world_reported = (torch.distributed.get_world_size()
+                      if torch.distributed.is_available() and torch.distributed.is_initialized() else 1)
+    sec_steps = max(10, args.steps // 2)  # the configs[2] / configs[3] legs
 
     # ---------------- secondary: report latency at 4096 ranks (strong) ---------------
     lat = None
     if not args.no_latency4096:
         del r["ns"]
         torch.cuda.empty_cache()
-        r4 = run_config(C3, C3["K"], max(3, args.steps // 4), 2, world, rank, dev, time_kernel=True,
+        r4 = run_config(C3, C3["K"], sec_steps, 3, world, rank, dev, time_kernel=True,
                         use_graph=not args.no_graph)
         t4 = allreduce(r4["elapsed"], torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
         tot4 = allreduce(float(r4["samples"]), torch.distributed.ReduceOp.SUM if world > 1 else None,
                          world, dev)
-        n4 = max(3, args.steps // 4)
+        n4 = sec_steps
         s4 = r4["res"]
         k4 = comm_max(r4["kern_ms"], world, dev)
         lat = dict(ranks=C3["R"], kernels=C3["K"], samples_per_kernel=C3["s_push"],
                    ms_per_report=t4 / n4 * 1e3, samples_per_s=tot4 * n4 / t4,
                    stats_kernel_ms=k4,
                    stats_kernel_hbm_frac=(4 * r4["samples"] + 24 * r4["nseg"]) / (k4 * 1e-3) / HBM_PEAK,
-                   straggler_sets_exact=bool(np.array_equal(
-                       s4.stragglers_relative, synth.straggler_ranks(C3["R"]).astype(bool))))
+                   steps=n4, kernels_per_rank=shard_sizes(C3["K"], world),
+                   straggler_sets_exact=all_ranks(bool(np.array_equal(
+                       s4.stragglers_relative, synth.straggler_ranks(C3["R"]).astype(bool))), world, dev))
         if world == 1 and rank == 0 and not args.no_cpu_baseline:
             # the north_star's >= 100x target is stated at this configuration
             cb4 = cpu_baseline(r4["ns"], r4["kidx"], C3, r4["rep"].stats, args.cpu4096_ranks,
@@ -357,7 +378,7 @@ def main():
     zipf = None
     if not args.no_zipf:
         torch.cuda.empty_cache()
-        zipf = run_zipf(max(3, args.steps // 4), 2, world, rank, dev,
+        zipf = run_zipf(sec_steps, 3, world, rank, dev,
                         0 if args.no_cpu_baseline else args.zipf_cpu_ranks, threads)
         torch.cuda.empty_cache()
 
@@ -427,7 +448,9 @@ def main():
                        "ranks": C2["R"], "kernels_per_gpu": C2["K"], "kernels_total": K_global,
                        "samples_pushed": C2["s_push"], "ring_cap": C2["cap"],
                        "parallelism": f"kernel-hash shards x{world}" if world > 1 else "1 GPU",
-                       "world_size": world, "backend": backend or "none (1 GPU)",
+                       "world_size": world, "world_size_reported": world_reported,
+                       "kernels_per_rank": shard_sizes(K_global, world),
+                       "backend": backend or "none (1 GPU)",
                        "stats_mode": "fast", "launch": "eager" if args.no_graph else "hip_graph"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,

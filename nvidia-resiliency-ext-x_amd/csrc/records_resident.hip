@@ -48,7 +48,9 @@ constexpr int RR_WAVES = 8;
 constexpr int RR_THREADS = 64 * RR_WAVES;
 constexpr int RR_PPL = 47;  // record pairs (16 B) per lane held in VGPRs: 188 of 256
 constexpr int64_t RR_CAPACITY = (int64_t)RR_PPL * 2 * RR_THREADS;
-constexpr int RR_LANE_MAX = 16;  // buckets of up to this many records: one lane each
+constexpr int RR_LANE_MAX = 16;    // buckets of up to this many records: one lane each
+constexpr int RR_LANE_FINAL = 64;  // ... in the last group (the stream's registers freed)
+constexpr int RR_SLOT_BITS = 13;   // register keys: bucket start << 13 | slot (nslots < 8192)
 constexpr int RR_NB = 256;       // histogram bins per wave (Bins<16>, hist_locate1<16>)
 constexpr uint32_t RR_OVF = 0x80000000u;
 constexpr size_t RR_LDS = 160 * 1024 - 256;  // one workgroup per CU takes the whole LDS
@@ -245,8 +247,8 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
     uint32_t* wlist = lds + 3 * nslots;    // [nslots] the group's wave-path slots
     uint32_t* hists = lds + ((4 * nslots + 3) & ~(int64_t)3);  // [RR_WAVES][RR_NB]
     uint32_t* stage = hists + RR_WAVES * RR_NB;                 // [stg] the group's buckets
-    __shared__ uint32_t wtot[RR_WAVES];
-    __shared__ uint32_t sh_hi, sh_wl, sh_q, sh_total, sh_ovf;
+    __shared__ uint32_t wtot[2][RR_WAVES];
+    __shared__ uint32_t sh_next, sh_wl, sh_q, sh_total, sh_ta, sh_ovf;
 
     const int64_t t = blockIdx.x;
     const int tid = threadIdx.x;
@@ -302,36 +304,56 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
     }
     __syncthreads();
 
-    // ---- scan over slots: padded keeps, each wave its own chunk of slots (chunk totals
-    // first, then each wave scans its chunk from the preceding totals)
+    // ---- scan over slots: padded keeps laid out in two tiers -- tier A (keep > RR_LANE_FINAL)
+    // first, tier B (the buckets a lane reduces) after it, slot order inside a tier, each bucket
+    // padded to 4 records.  Tier B starts an LDS group of its own, so when it fits one stage it
+    // is the LAST group, reduced after the last placement has freed the stream's registers
+    // (lane classes up to 64 records there).  Each wave scans its own chunk of slots: chunk
+    // totals first, then each wave from the preceding totals.
     const auto keep_of = [&](uint32_t c) { return (cap > 0 && c > (uint32_t)cap) ? (uint32_t)cap : c; };
+    const auto tier_b = [](uint32_t keep) { return keep <= (uint32_t)RR_LANE_FINAL; };
     const int64_t chunk = ((nslots + RR_WAVES - 1) / RR_WAVES + 63) & ~(int64_t)63;
     const int64_t c_lo = min(nslots, chunk * wave), c_hi = min(nslots, c_lo + chunk);
     {
-        uint32_t p = 0;
-        for (int64_t s = c_lo + lane; s < c_hi; s += 64) p += (keep_of(cnt[s]) + 3u) & ~3u;
-        p = wave_sum_u32(p);
-        if (lane == 0) wtot[wave] = p;
+        uint32_t pa = 0, pb = 0;
+        for (int64_t s = c_lo + lane; s < c_hi; s += 64) {
+            const uint32_t k = keep_of(cnt[s]);
+            const uint32_t p = (k + 3u) & ~3u;
+            pa += tier_b(k) ? 0u : p;
+            pb += tier_b(k) ? p : 0u;
+        }
+        pa = wave_sum_u32(pa);
+        pb = wave_sum_u32(pb);
+        if (lane == 0) {
+            wtot[0][wave] = pa;
+            wtot[1][wave] = pb;
+        }
     }
     __syncthreads();
     {
-        uint32_t carry = 0, total = 0;
+        uint32_t ca = 0, cb = 0, ta = 0, tb = 0;
         for (int v = 0; v < RR_WAVES; ++v) {
-            carry += v < wave ? wtot[v] : 0u;
-            total += wtot[v];
+            ca += v < wave ? wtot[0][v] : 0u;
+            cb += v < wave ? wtot[1][v] : 0u;
+            ta += wtot[0][v];
+            tb += wtot[1][v];
         }
+        cb += ta;  // tier B follows tier A
         bool ovf = false;
         for (int64_t c0 = c_lo; c0 < c_hi; c0 += 64) {
             const int64_t s = c0 + lane;
+            const bool valid = s < c_hi;
             uint32_t c = 0, keep = 0;
-            if (s < c_hi) {
+            if (valid) {
                 c = cnt[s];
                 keep = keep_of(c);
             }
+            const bool b = tier_b(keep);
             const uint32_t padded = (keep + 3u) & ~3u;
-            const uint32_t incl = wave_incl_scan_u32(padded);
-            if (s < c_hi) {
-                const uint32_t start = carry + incl - padded;
+            const uint32_t ia = wave_incl_scan_u32(valid && !b ? padded : 0u);
+            const uint32_t ib = wave_incl_scan_u32(valid && b ? padded : 0u);
+            if (valid) {
+                const uint32_t start = b ? cb + ib - padded : ca + ia - padded;
                 const bool o2 = keep != c;
                 ovf |= o2;
                 st[s] = start | (o2 ? RR_OVF : 0u);
@@ -340,58 +362,64 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
                 counts[g] = (int32_t)c;
                 seg_len[g] = (int32_t)keep;
             }
-            carry += rl(incl, 63);
+            ca += rl(ia, 63);
+            cb += rl(ib, 63);
         }
         if (__ballot(ovf) != 0 && lane == 0) atomicOr(&sh_ovf, 1u);
-        if (tid == 0) sh_total = total;
+        if (tid == 0) {
+            sh_total = ta + tb;
+            sh_ta = ta;
+        }
     }
     __syncthreads();
-
-    RR_TRACE("rr: scanned total=%u ovf=%u\n", sh_total, sh_ovf);
+    RR_TRACE("rr: scanned total=%u tierA=%u ovf=%u\n", sh_total, sh_ta, sh_ovf);
     const auto start_of = [&](int64_t s) { return st[s] & ~RR_OVF; };
-    for (int64_t lo = 0; lo < nslots;) {
-        // ---- the group: the longest run of slots from lo whose buckets fit the stage
-        if (tid == 0) {
-            const uint32_t lim = start_of(lo) + (uint32_t)stg;
-            const uint32_t total = sh_total;
-            const auto end_of = [&](int64_t s) { return s + 1 < nslots ? start_of(s + 1) : total; };
-            int64_t a = lo + 1, b = nslots;  // end_of(a - 1) <= lim (a bucket fits the stage)
-            while (a < b) {
-                const int64_t m = (a + b + 1) >> 1;
-                if (end_of(m - 1) <= lim) a = m;
-                else b = m - 1;
-            }
-            sh_hi = (uint32_t)a;
-            sh_wl = 0u;
-            sh_q = 0u;
+
+    // ---- register keys: (bucket start << RR_SLOT_BITS) | slot, so that a group (a window of
+    // bucket starts) is one subtract and compare per record (host: nslots < 2^RR_SLOT_BITS,
+    // starts < 2^(32 - RR_SLOT_BITS) for a resident stream)
+    if (resident) {
+#pragma unroll
+        for (int u = 0; u < RR_PPL; ++u) {
+            if (w[u].x != 0xFFFFFFFFu) w[u].x = (start_of(w[u].x) << RR_SLOT_BITS) | w[u].x;
+            if (w[u].z != 0xFFFFFFFFu) w[u].z = (start_of(w[u].z) << RR_SLOT_BITS) | w[u].z;
         }
-        __syncthreads();
-        const int64_t hi = sh_hi;
-        RR_TRACE("rr: group [%ld, %ld)\n", (long)lo, (long)hi);
-        const uint32_t P = start_of(lo);
-        const uint32_t span = (uint32_t)(hi - lo);
-        const uint32_t lo32 = (uint32_t)lo;
+    }
+
+    const uint32_t total = sh_total, ta = sh_ta;
+    constexpr uint32_t SLOT_MASK = (1u << RR_SLOT_BITS) - 1u;
+    // one LDS group: the buckets starting in [P, P + W); last: the final one, whose buckets of
+    // RR_LANE_MAX+1 .. RR_LANE_FINAL records are left to the lane pass after the group loop
+    // (the stream's registers are dead there; inside the loop they would have to stay live)
+    const auto group = [&](bool last, uint32_t P, uint32_t W) {
         const auto place = [&](uint32_t s, uint32_t x) {
-            if (s - lo32 < span) {
+            if (start_of(s) - P < W) {
                 const uint32_t pos = atomicAdd(&cur[s], 1u);
                 if (!(pos & RR_OVF)) stage[pos - P] = x;
             }
         };
         if (NVRX_AB_RR & 4) {
         } else if (resident) {
-            // branch-free batches: the cursor atomics of RR_PB pairs are issued back to back
-            // (a record outside the group increments this lane's dummy word), then their
-            // stores (outside the group / overflowed: this lane's second dummy word)
+            // branch-free batches: the cursor atomics of RR_PB pairs are issued back to back (a
+            // record outside the group increments this lane's dummy word), then their stores
+            // (outside the group / overflowed: this lane's second dummy word)
             constexpr int RR_PB = 4;
+            // an opaque copy of the slot mask, made inside the group loop: with a constant mask
+            // the compiler proves (key - (P << 13)) & mask == key & mask and hoists the 94 masked
+            // keys out of the loop, which spilled the stream's registers
+            uint32_t slot_mask = SLOT_MASK;
+            asm volatile("" : "+s"(slot_mask));
 #pragma unroll
             for (int u0 = 0; u0 < RR_PPL; u0 += RR_PB) {
                 uint32_t pos[2 * RR_PB];
                 bool in[2 * RR_PB];
 #pragma unroll
                 for (int k = 0; k < 2 * RR_PB && u0 + k / 2 < RR_PPL; ++k) {
-                    const uint32_t sl = (k & 1) ? w[u0 + k / 2].z : w[u0 + k / 2].x;
-                    in[k] = sl - lo32 < span;
-                    pos[k] = atomicAdd(in[k] ? cur + sl : dummy, 1u);
+                    const uint32_t key = (k & 1) ? w[u0 + k / 2].z : w[u0 + k / 2].x;
+                    // start - P < W  <=>  key - (P << 13) < W << 13 (the slot bits lie below)
+                    const uint32_t dk = key - (P << RR_SLOT_BITS);
+                    in[k] = dk < (W << RR_SLOT_BITS);  // invalid keys (all ones) never fall inside
+                    pos[k] = atomicAdd(in[k] ? cur + (dk & slot_mask) : dummy, 1u);
                 }
 #pragma unroll
                 for (int k = 0; k < 2 * RR_PB && u0 + k / 2 < RR_PPL; ++k) {
@@ -411,14 +439,15 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
             // occurrences >= count - keep (the ring's last `cap`), as records_bucket_kernel
             __syncthreads();
             if (wave == 0) {
-                for (int64_t s = lo + lane; s < hi; s += 64)
-                    if (st[s] & RR_OVF) cur[s] = 0u;
+                for (int64_t s = lane; s < nslots; s += 64)
+                    if ((st[s] & RR_OVF) && start_of(s) - P < W) cur[s] = 0u;
                 __builtin_amdgcn_wave_barrier();
                 for (int64_t b = 0; b < n; b += 64) {
                     const int64_t i = b + lane;
                     nvrx_record rec = {0xFFFFFFFFu, 0u};
                     if (i < n) rec = rs[i];
-                    const bool ok = rec.slot - lo32 < span && (st[rec.slot] & RR_OVF);
+                    bool ok = rec.slot < ns32;
+                    if (ok) ok = (st[rec.slot] & RR_OVF) && start_of(rec.slot) - P < W;
                     uint64_t pending = __ballot(ok);
                     uint32_t occ = 0;
                     while (pending) {
@@ -433,8 +462,8 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
                         pending &= ~grp;
                     }
                     if (ok) {
-                        const uint32_t total = cnt[rec.slot];
-                        const uint32_t drop = total - keep_of(total);
+                        const uint32_t c = cnt[rec.slot];
+                        const uint32_t drop = c - keep_of(c);
                         if (occ >= drop) stage[start_of(rec.slot) - P + (occ - drop)] = rec.ns;
                     }
                 }
@@ -443,20 +472,23 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
         __syncthreads();
 
         // ---- statistics of the group's buckets: short ones one lane each, the rest queued
-        for (int64_t s = lo + tid; s < hi; s += RR_THREADS) {
-            const uint32_t keep = keep_of(cnt[s]);
+        const uint32_t lane_max = last ? (uint32_t)RR_LANE_FINAL : (uint32_t)RR_LANE_MAX;
+        for (int64_t s = tid; s < nslots; s += RR_THREADS) {
+            const uint32_t b = start_of(s);
+            const bool mine = b - P < W;
+            const uint32_t keep = mine ? keep_of(cnt[s]) : 0u;
             const int64_t g = t * nslots + s;
-            const uint32_t* bk = stage + (start_of(s) - P);
-            const bool wave_path = keep > (uint32_t)RR_LANE_MAX && !(NVRX_AB_RR & 1);
-            if (NVRX_AB_RR & 2) {
+            const uint32_t* bk = stage + (b - P);
+            const bool wave_path = mine && keep > lane_max && !(NVRX_AB_RR & 1);
+            if ((NVRX_AB_RR & 2) || !mine) {
             } else if (keep == 0) {
                 write_empty(out, g);
             } else if (keep <= 8) {
                 lane_bucket<8, 1>(bk, (int)keep, g, out);
-            } else if (!wave_path) {
+            } else if (keep <= 16) {
                 lane_bucket<16, 9>(bk, (int)keep, g, out);
             }
-            const uint64_t bm = __ballot(wave_path);
+        const uint64_t bm = __ballot(wave_path);
             uint32_t base = 0;
             if (lane == __builtin_ffsll(bm) - 1) base = atomicAdd(&sh_wl, (uint32_t)__popcll(bm));
             base = __builtin_amdgcn_readlane(base, __builtin_ffsll(bm | (1ull << 63)) - 1);
@@ -464,7 +496,7 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
         }
         __syncthreads();
         const uint32_t nwl = sh_wl;
-        RR_TRACE("rr: lane stats done, %u wave-path buckets\n", nwl);
+        RR_TRACE("rr: group [%u, +%u) last=%d: %u wave-path buckets\n", P, W, (int)last, nwl);
         for (;;) {
             uint32_t j = 0;
             if (lane == 0) j = atomicAdd(&sh_q, 1u);
@@ -474,7 +506,42 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
             lds_wave_stats(stage + (start_of(s) - P), (int)keep_of(cnt[s]), t * nslots + s, hist, out);
         }
         __syncthreads();
-        lo = hi;
+    };
+
+    uint32_t P = 0, W = 0;
+    for (;;) {
+        // the next group boundary: the start of the first bucket (layout order) that does not fit
+        // a stage opened at P, and the start of tier B (it opens a group of its own)
+        if (tid == 0) {
+            sh_next = P < ta ? ta : 0xFFFFFFFFu;
+            sh_wl = 0u;
+            sh_q = 0u;
+        }
+        __syncthreads();
+        for (int64_t s = tid; s < nslots; s += RR_THREADS) {
+            const uint32_t k = keep_of(cnt[s]);
+            const uint32_t b = start_of(s);
+            if (k > 0 && b >= P && b + ((k + 3u) & ~3u) - P > (uint32_t)stg) atomicMin(&sh_next, b);
+        }
+        __syncthreads();
+        const uint32_t Pn = sh_next;
+        const bool last = Pn >= total;
+        W = last ? total - P + 1 : Pn - P;  // + 1: empty buckets start at `total` too
+        group(last, P, W);
+        if (last) break;
+        P = Pn;
+    }
+    // ---- the last group's buckets of RR_LANE_MAX+1 .. RR_LANE_FINAL records, one lane each,
+    // still in the stage (tier B: all of them when it fits one stage)
+    if (!(NVRX_AB_RR & 2)) {
+        for (int64_t s = tid; s < nslots; s += RR_THREADS) {
+            const uint32_t b = start_of(s);
+            const uint32_t keep = b - P < W ? keep_of(cnt[s]) : 0u;
+            if (keep <= (uint32_t)RR_LANE_MAX || keep > (uint32_t)RR_LANE_FINAL) continue;
+            const uint32_t* bk = stage + (b - P);
+            if (keep <= 32) lane_bucket<32, 17>(bk, (int)keep, t * nslots + s, out);
+            else lane_bucket<64, 33>(bk, (int)keep, t * nslots + s, out);
+        }
     }
 }
 
@@ -483,7 +550,8 @@ hipError_t records_resident_stats(const nvrx_record* recs, const int64_t* rec_of
                                   const nvrx_stats_soa& out, hipStream_t st) {
     if (nstreams <= 0 || nslots <= 0) return hipSuccess;
     const int64_t stg = records_resident_stage(nslots);
-    if (cap <= 0 || ((cap + 3) & ~(int64_t)3) > stg) return hipErrorInvalidValue;
+    if (cap <= 0 || ((cap + 3) & ~(int64_t)3) > stg || nslots >= ((int64_t)1 << RR_SLOT_BITS))
+        return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute((const void*)records_resident_kernel,

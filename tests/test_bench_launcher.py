@@ -43,3 +43,26 @@ def test_launcher_two_ranks_gloo_rehearsal():
     assert line["straggler_sets_exact"] is True
     assert line["latency_4096_ranks"]["straggler_sets_exact"] is True
     assert 0 < line["roofline"]["frac"] < 1.5
+
+
+def test_launcher_four_ranks_dry_run():
+    line = _run(["--gpus", "4", "--dry-run"], timeout=300)
+    assert line == {"dry_run": True, "n_gpus": 4, "world_size": 4, "backend": "gloo"}
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_launcher_four_ranks_gloo_rehearsal():
+    # the N > 1 line as the driver's 8-GPU node will print it, rehearsed with
+    # 4 ranks on the one GPU over gloo: the world size the process group reports, the kernel
+    # shard of every rank, and exact straggler sets (on every rank) for all three legs
+    line = _run(["--gpus", "4", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
+    cfg = line["config"]
+    assert line["n_gpus"] == 4 and cfg["world_size"] == 4 and cfg["world_size_reported"] == 4
+    assert cfg["backend"] == "gloo" and cfg["kernels_total"] == 4 * 2048
+    assert sum(cfg["kernels_per_rank"]) == 4 * 2048 and len(cfg["kernels_per_rank"]) == 4
+    assert min(cfg["kernels_per_rank"]) > 0
+    assert line["straggler_sets_exact"] is True
+    lat, zipf = line["latency_4096_ranks"], line["zipf_16384_ranks"]
+    assert lat["straggler_sets_exact"] is True and sum(lat["kernels_per_rank"]) == 2048
+    assert zipf["straggler_sets_exact"] is True and sum(zipf["kernels_per_rank"]) == 2048
