@@ -38,8 +38,14 @@
 #endif
 #ifdef RR_DEBUG
 #define RR_TRACE(...) do { if (blockIdx.x == 0 && threadIdx.x == 0) printf(__VA_ARGS__); } while (0)
+// progress words in host-mapped memory, polled by tools/rr_debug.hip while the kernel runs:
+// [wave] = last phase reached by wave `wave` of block 0, [8 + wave] = a value of that phase
+__device__ uint32_t* rr_dbg_ptr;
+#define RR_MARK(phase, val) do { if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && rr_dbg_ptr) { \
+    rr_dbg_ptr[threadIdx.x >> 6] = (phase); rr_dbg_ptr[8 + (threadIdx.x >> 6)] = (val); __threadfence_system(); } } while (0)
 #else
 #define RR_TRACE(...) do {} while (0)
+#define RR_MARK(phase, val) do {} while (0)
 #endif
 
 namespace nvrx {
@@ -83,8 +89,8 @@ __device__ __forceinline__ void lds_walk(const uint32_t* seg, int n, F&& f) {
 
 // One wave: FAST statistics of seg[0:n) (n >= 1) held in LDS -- lean_body's algorithm with the
 // samples re-read from LDS at every pass instead of held in registers (the registers hold the
-// record stream).  hist: this wave's RR_NB words of LDS.
-__device__ __forceinline__ void lds_wave_stats(const uint32_t* seg, int n, int64_t g, uint32_t* hist,
+// record stream).  hist: this wave's RR_NB words of LDS.  Returns MAX (a key).
+__device__ __forceinline__ unsigned lds_wave_stats(const uint32_t* seg, int n, int64_t g, uint32_t* hist,
                                             const nvrx_stats_soa& out) {
     constexpr int LOGNB = 8;
     constexpr int BPL = RR_NB / 64;
@@ -99,6 +105,7 @@ __device__ __forceinline__ void lds_wave_stats(const uint32_t* seg, int n, int64
     const unsigned mn = wave_min_b(lmn);
     const unsigned mx = wave_max_b(lmx);
     const unsigned range = mx - mn;
+    RR_MARK(100, n);
     // exact sum of d = x - MIN; squares about a pivot c (a sample) in f64; c = 0 once the
     // range reaches 2^31 (d - c must be a signed 32-bit value)
     unsigned c = seg[0] - mn;
@@ -125,11 +132,13 @@ __device__ __forceinline__ void lds_wave_stats(const uint32_t* seg, int n, int64
     __builtin_amdgcn_wave_barrier();
     const double sd = wave_sum_f64_b((double)(((uint64_t)shi << 32) | slo));
     const double sq = wave_sum_f64_b(acc);
+    RR_MARK(101, shift);
 
     const unsigned t0 = (unsigned)((n & 1) ? n / 2 : n / 2 - 1);
     const unsigned t1 = (unsigned)(n / 2);
     unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
-    for (int level = 0;; ++level) {
+    for (int level = 0; level < 8; ++level) {  // <= 4 levels of 8 bits (bound: every wave exits)
+        RR_MARK(110 + level, wlo);
         if (level > 0) {
 #pragma unroll
             for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
@@ -204,20 +213,28 @@ __device__ __forceinline__ void lds_wave_stats(const uint32_t* seg, int n, int64
         shift = shift > LOGNB ? shift - LOGNB : 0;
     }
     emit_stats(out, g, n, mn, mx, d0, d1, sd, sq, c, ColRef{});
-    if (mx >= NVRX_KEY_WIDE) {  // keys of >= 3.76 s: moments of the decoded values (rare)
-        double a = 0.0;
-        lds_walk(seg, n, [&](unsigned x, bool ok) { a += ok ? (double)key_to_f32(x) : 0.0; });
-        const double mean = wave_sum_f64(a) / (double)n;
-        double q = 0.0;
-        lds_walk(seg, n, [&](unsigned x, bool ok) {
-            const double e = (double)key_to_f32(x) - mean;
-            q = ok ? __builtin_fma(e, e, q) : q;
-        });
-        const double var = wave_sum_f64(q) / (double)n;
-        if (lane == 0) {
-            out.avg[g] = (float)(mean / 1000.0);
-            out.std[g] = (float)(__builtin_sqrt(var) / 1000.0);
-        }
+    return mx;
+}
+
+// Keys of >= 3.76 s in a wave-path bucket (rare): lane 0 overwrites AVG / STD with the mean and
+// population std of the decoded f32(ns) values in f64, each rounded once (the integer sums of
+// lds_wave_stats do not apply to f32-valued keys).  A separate call after lds_wave_stats
+// returns: placed inside it, after its median search, the branch hung the wave (gfx950 build of
+// ROCm 7.2: control flow merged into the search loop's exits).
+__device__ __noinline__ void lds_wide_moments(const uint32_t* seg, int n, int64_t g, const nvrx_stats_soa& out) {
+    const int lane = lane_id();
+    double a = 0.0;
+    for (int i = lane; i < n; i += 64) a += (double)key_to_f32(seg[i]);
+    const double mean = wave_sum_f64(a) / (double)n;
+    double q = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        const double e = (double)key_to_f32(seg[i]) - mean;
+        q = __builtin_fma(e, e, q);
+    }
+    const double var = wave_sum_f64(q) / (double)n;
+    if (lane == 0) {
+        out.avg[g] = (float)(mean / 1000.0);
+        out.std[g] = (float)(__builtin_sqrt(var) / 1000.0);
     }
 }
 
@@ -281,6 +298,7 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
     for (int64_t s = tid; s < nslots; s += RR_THREADS) cnt[s] = 0u;
     if (tid == 0) sh_ovf = 0u;
     RR_TRACE("rr: block 0 n=%ld resident=%d o=%d\n", (long)n, (int)resident, o);
+    RR_MARK(1, (uint32_t)n);
     __syncthreads();
 
     // ---- count: branch-free -- an invalid record adds to this lane's own word of the wave's
@@ -373,6 +391,7 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
     }
     __syncthreads();
     RR_TRACE("rr: scanned total=%u tierA=%u ovf=%u\n", sh_total, sh_ta, sh_ovf);
+    RR_MARK(2, sh_total);
     const auto start_of = [&](int64_t s) { return st[s] & ~RR_OVF; };
 
     // ---- register keys: (bucket start << RR_SLOT_BITS) | slot, so that a group (a window of
@@ -496,6 +515,7 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
         }
         __syncthreads();
         const uint32_t nwl = sh_wl;
+        RR_MARK(3, nwl);
         RR_TRACE("rr: group [%u, +%u) last=%d: %u wave-path buckets\n", P, W, (int)last, nwl);
         for (;;) {
             uint32_t j = 0;
@@ -503,8 +523,12 @@ void records_resident_kernel(const nvrx_record* __restrict__ recs, const int64_t
             j = __builtin_amdgcn_readfirstlane(j);
             if (j >= nwl) break;
             const int64_t s = wlist[j];
-            lds_wave_stats(stage + (start_of(s) - P), (int)keep_of(cnt[s]), t * nslots + s, hist, out);
+            const uint32_t* seg = stage + (start_of(s) - P);
+            const int kn = (int)keep_of(cnt[s]);
+            if (lds_wave_stats(seg, kn, t * nslots + s, hist, out) >= NVRX_KEY_WIDE)
+                lds_wide_moments(seg, kn, t * nslots + s, out);
         }
+        RR_MARK(4, 0);
         __syncthreads();
     };
 
