@@ -46,13 +46,6 @@ hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_
 // dst[i] = src[i] with every slot >= nslots replaced by UINT32_MAX (never counted)
 hipError_t records_ingest(nvrx_record* dst, const nvrx_record* src, int64_t n, uint32_t nslots,
                           hipStream_t st);
-// FAST statistics of record streams without materialised buckets (records_resident.hip): one
-// workgroup per stream holds it on chip.  records_resident_stage(nslots) = LDS words left for
-// the bucket stage; the call needs 0 < cap and round4(cap) <= that.
-int64_t records_resident_stage(int64_t nslots);
-hipError_t records_resident_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
-                                  int64_t nslots, int64_t cap, int32_t* seg_len, int32_t* counts,
-                                  const nvrx_stats_soa& out, hipStream_t st);
 hipError_t records_unbucket(const int64_t* seg_off, const int32_t* seg_len, const int64_t* dst_off,
                             const uint32_t* ns, int64_t nslots, nvrx_record* out, hipStream_t st);
 

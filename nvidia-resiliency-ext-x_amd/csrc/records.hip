@@ -434,14 +434,6 @@ hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_
                          int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                          const nvrx_stats_soa& out, uint32_t* col_ref, hipStream_t st) {
-    // FAST mode with a ring that fits the LDS stage: one pass over the streams, no buckets
-    // (records_resident.hip)
-    if (mode == NVRX_STATS_FAST && cap > 0 && nslots < 8192 &&
-        ((cap + 3) & ~(int64_t)3) <= records_resident_stage(nslots)) {
-        hipError_t e = records_resident_stats(recs, rec_off, nstreams, nslots, cap, seg_len, counts, out, st);
-        if (e != hipSuccess || !col_ref) return e;
-        return kernel_ref(out.num, out.med, nstreams, nslots, nullptr, col_ref, st);
-    }
     hipError_t e = records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off, seg_len, out_ns,
                                   counts, st, &out);
     if (e != hipSuccess) return e;
