@@ -212,7 +212,10 @@ int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t 
                        int64_t nslots, int64_t cap, int32_t mode, int64_t max_len, int64_t* seg_off,
                        int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                        const nvrx_stats_soa* out, uint32_t* col_ref, void* stream);
-/* Largest nslots nvrx_records_bucket accepts (per-slot counters live in LDS). */
+/* Slots one bucketing pass counts (its per-slot counters live in LDS).  Any nslots is accepted:
+ * a larger slot table is bucketed in passes over ranges of this many slots, each re-reading the
+ * streams (the reference's per-kernel map is unbounded, CuptiProfiler.cpp:189-198);
+ * nvrx_records_bucket_capacity accounts for the passes' regions of out_ns. */
 int64_t nvrx_records_max_slots(void);
 
 /* ---------------------------------------------------------------- profiler handle */

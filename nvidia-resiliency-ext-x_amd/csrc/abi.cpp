@@ -197,7 +197,6 @@ int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t 
                        int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                        const nvrx_stats_soa* out, uint32_t* col_ref, void* stream) {
     NVRX_CHECK_ARG(nstreams >= 0 && nslots >= 0 && max_len >= 0, "nvrx_records_stats: negative size");
-    NVRX_CHECK_ARG(nslots <= nvrx_records_max_slots(), "nvrx_records_stats: too many slots");
     NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
                    "nvrx_records_stats: null output array");
     NVRX_CHECK_ARG(nstreams == 0 || nslots == 0 ||
@@ -220,7 +219,6 @@ int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t
                         int64_t nslots, int64_t cap, int64_t* seg_off, int32_t* seg_len,
                         uint32_t* out_ns, int32_t* counts, void* stream) {
     NVRX_CHECK_ARG(nstreams >= 0 && nslots >= 0, "nvrx_records_bucket: negative size");
-    NVRX_CHECK_ARG(nslots <= nvrx_records_max_slots(), "nvrx_records_bucket: too many slots");
     NVRX_CHECK_ARG(nstreams == 0 || nslots == 0 ||
                        (rec_off && seg_off && seg_len && out_ns && counts),
                    "nvrx_records_bucket: null array");
@@ -410,8 +408,7 @@ int flush_locked(nvrx_profiler* p) {
     const int64_t nslots = (int64_t)p->names.size();
     const int64_t cap = p->cfg.stats_max_len_per_kernel;
     const int64_t retain_bound = nslots * (cap > 0 ? cap : p->log_n);
-    if (cap > 0 && p->log_n > (int64_t)1 << 22 && p->log_n > 4 * retain_bound &&
-        nslots <= nvrx_records_max_slots()) {
+    if (cap > 0 && p->log_n > (int64_t)1 << 22 && p->log_n > 4 * retain_bound) {
         // compaction keeps exactly the records a later retention step could still keep
         Work w;
         int rc = bucket_log(p, nslots, /*force_stable=*/1, w);
@@ -443,6 +440,28 @@ int flush_locked(nvrx_profiler* p) {
     }
     return NVRX_OK;
 }
+
+// While the live capture is started, a report pauses it: the dispatch context is stopped
+// (~10 us) before the flush and the device work and started again after, so the report's own
+// kernels (bucketing, statistics, copies) are not captured as dispatches of the profiled job --
+// the reference's getStats runs on the host and adds nothing.  It does not make the flush
+// cheaper: rocprofiler_flush_buffer takes ~3.5-5 ms whenever records are pending, started or
+// stopped, and ~30 us when none are (tools/capture_cost.cpp, profiles/r03/capture_cost.json).
+struct CapturePause {
+    nvrx_profiler* p;
+    bool paused = false;
+    explicit CapturePause(nvrx_profiler* q) : p(q) {
+        bool started;
+        {
+            std::lock_guard<std::mutex> lk(p->mu);
+            started = p->started;
+        }
+        if (started && nvrx::capture_ready()) paused = nvrx::capture_stop(p) == 0;
+    }
+    ~CapturePause() {
+        if (paused) (void)nvrx::capture_start(p);
+    }
+};
 
 uint32_t slot_of_name(nvrx_profiler* p, const std::string& key) {
     auto it = p->name_to_slot.find(key);
@@ -587,6 +606,7 @@ int nvrx_profiler_stop(nvrx_profiler* p) {
 
 int nvrx_profiler_reset(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_reset: null handle");
+    CapturePause pause(p);
     (void)nvrx::capture_flush();  // CuptiProfiler.cpp:149: flush, then clear (outside the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);
@@ -671,6 +691,7 @@ int nvrx_profiler_saturated(nvrx_profiler* p, int64_t* count) {
 int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
                             int32_t* num, float* mn, float* mx, float* med, float* avg, float* sd) {
     NVRX_CHECK_ARG(p && count && cap_out >= 0, "nvrx_profiler_get_stats: bad arguments");
+    CapturePause pause(p);  // the report's own kernels are not captured
     (void)nvrx::capture_flush();  // CuptiProfiler.cpp:138 cuptiActivityFlushAll (before the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);
@@ -683,10 +704,6 @@ int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, u
         p->c_num.clear();
         const int64_t nslots = (int64_t)p->names.size();
         if (p->log_n > 0 && nslots > 0) {
-            if (nslots > nvrx_records_max_slots())
-                return fail(NVRX_ERR_INVALID,
-                            "nvrx_profiler_get_stats: more distinct kernels in one report interval "
-                            "than nvrx_records_max_slots()");
             Work w;
             rc = bucket_log(p, nslots, 0, w);
             if (rc) return rc;
@@ -744,6 +761,7 @@ int nvrx_profiler_get_records(nvrx_profiler* p, int64_t cap_out, int64_t* count,
                               nvrx_record* out) {
     NVRX_CHECK_ARG(p && count && cap_out >= 0 && (cap_out == 0 || out),
                    "nvrx_profiler_get_records: bad arguments");
+    CapturePause pause(p);
     (void)nvrx::capture_flush();
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);

@@ -36,6 +36,10 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 }
 
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
+// Slots one bucketing pass counts in LDS; a larger slot table is bucketed in passes over
+// consecutive slot ranges (each pass re-reads the streams and ignores other slots' records),
+// each pass into its own region of out_ns.
+constexpr int64_t RB_PASS_SLOTS = NVRX_RECORDS_MAX_LDS / (3 * sizeof(uint32_t));
 constexpr int RB_TINY = 8;  // records_stats: buckets this short are reduced by the bucketing kernel
 
 // records [lo, hi) of a stream in 16-byte pairs where the base allows it; f(rec) per record.
@@ -102,7 +106,7 @@ void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
     int32_t* counts, int64_t stash_pairs, int64_t stage_cap, uint32_t cold_max,
-    nvrx_stats_soa tiny) {
+    nvrx_stats_soa tiny, uint32_t slot_lo, int64_t seg_stride, int pass) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
@@ -122,6 +126,10 @@ void records_bucket_kernel(
     const nvrx_record* rs = recs + r0;
     const int64_t n = r1 - r0;
     const int64_t base = stream_base(rec_off, t, nslots);
+    // a slot table larger than one pass's LDS counters: pass p's buckets follow the regions of
+    // passes 0..p-1, each as large as records_bucket_capacity's per-pass term
+    const int64_t ns_off = pass == 0 ? 0 :
+        (int64_t)pass * (((rec_off[gridDim.x] + 3) & ~(int64_t)3) + (int64_t)gridDim.x * stream_slack(RB_PASS_SLOTS));
     const bool pairs = (((uintptr_t)rs) & 15) == 0;
     // wave w's chunk: [lo, hi), even boundaries
     const int64_t per = ((n + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
@@ -143,7 +151,8 @@ void records_bucket_kernel(
     if (threadIdx.x == 0) any_ovf = force_stable ? 1u : 0u;
     __syncthreads();
     const auto count = [&](const nvrx_record& r) {
-        if (r.slot < (uint32_t)nslots) atomicAdd(&cnt[r.slot], 1u);
+        const uint32_t ls = r.slot - slot_lo;  // this pass's slots: [slot_lo, slot_lo + nslots)
+        if (ls < (uint32_t)nslots) atomicAdd(&cnt[ls], 1u);
     };
     if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
 #pragma unroll
@@ -238,8 +247,8 @@ void records_bucket_kernel(
                     const uint32_t flag = ovf || force_stable ? RB_OVF : 0u;
                     start[s] = st | flag;
                     cur[s] = flag ? RB_OVF : st;  // pass 2's write cursor (absolute in the stream)
-                    const int64_t g = t * nslots + s;
-                    seg_off[g] = base + st;
+                    const int64_t g = t * seg_stride + slot_lo + s;
+                    seg_off[g] = ns_off + base + st;
                     // a bucket this kernel reduces itself (after pass 2): a negative length
                     const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
                     seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
@@ -254,15 +263,16 @@ void records_bucket_kernel(
     // positions below stage_lim go to LDS (cold buckets only: an overflowed slot's walk
     // writes to memory directly)
     const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
-    uint32_t* out = out_ns + base;
+    uint32_t* out = out_ns + ns_off + base;
 
     // records of slots that kept everything: any order.  The cursor starts at the bucket's
     // start, so a record costs one returning LDS atomic (a lookup of start[] before the atomic
     // doubled the dependent LDS round trips: 4.5 -> 3.x ms on configs[3]); overflowed slots
     // hold RB_OVF, which the increments keep set, and are skipped here.
     const auto place = [&](const nvrx_record& r) {
-        if (r.slot < (uint32_t)nslots) {
-            const uint32_t pos = atomicAdd(&cur[r.slot], 1u);
+        const uint32_t ls = r.slot - slot_lo;
+        if (ls < (uint32_t)nslots) {
+            const uint32_t pos = atomicAdd(&cur[ls], 1u);
             if (pos < stage_lim)
                 stage[pos] = r.ns;
             else if (!(pos & RB_OVF))
@@ -327,7 +337,7 @@ void records_bucket_kernel(
                     const u32x4 a = sv[st / 4];
                     const u32x4 b = keep > 4 ? sv[st / 4 + 1] : u32x4{~0u, ~0u, ~0u, ~0u};
                     unsigned v[RB_TINY] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-                    lane_stats<RB_TINY>(v, (int)keep, t * nslots + s, tiny, ColRef{});
+                    lane_stats<RB_TINY>(v, (int)keep, t * seg_stride + slot_lo + s, tiny, ColRef{});
                 }
             }
         }
@@ -344,6 +354,7 @@ void records_bucket_kernel(
         const int64_t i = b + lane;
         nvrx_record rec = {0xFFFFFFFFu, 0u};
         if (i < n) rec = rs[i];
+        rec.slot -= slot_lo;  // this pass's local slot
         const bool ok = rec.slot < (uint32_t)nslots && (start[rec.slot] & RB_OVF);
         uint64_t pending = __ballot(ok);
         uint32_t occ = 0;
@@ -368,7 +379,12 @@ void records_bucket_kernel(
 }
 
 int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
-    return ((n + 3) & ~(int64_t)3) + nstreams * stream_slack(nslots);
+    int64_t c = 0;
+    for (int64_t lo = 0; lo < nslots; lo += RB_PASS_SLOTS) {
+        const int64_t m = std::min<int64_t>(RB_PASS_SLOTS, nslots - lo);
+        c += ((n + 3) & ~(int64_t)3) + nstreams * stream_slack(m);
+    }
+    return c;
 }
 
 // dynamic LDS of a bucketing launch: a single workgroup may take the whole 160 KiB of a CU
@@ -388,10 +404,11 @@ constexpr int RB_COLD = 512;     // largest cold bucket (records)
 constexpr int RB_WAVES = 16;
 constexpr int RB_REGS = RB_REGS_PER_BLOCK / (64 * RB_WAVES);
 
-hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
-                          int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
-                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
-                          const nvrx_stats_soa* tiny) {
+static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                                      int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
+                                      int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
+                                      const nvrx_stats_soa* tiny, uint32_t slot_lo, int64_t seg_stride,
+                                      int pass) {
     if (nstreams <= 0 || nslots <= 0) return hipSuccess;
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
@@ -423,8 +440,24 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
     }
     hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)nstreams), dim3(64 * RB_WAVES),
                        lds_launch, st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns,
-                       counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa);
+                       counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa, slot_lo, seg_stride, pass);
     return hipGetLastError();
+}
+
+hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
+                          int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
+                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
+                          const nvrx_stats_soa* tiny) {
+    // seg_off / seg_len / counts stay [nstreams][nslots]; pass p writes its slot range's columns
+    // and its buckets into out_ns after the regions of the passes before it
+    int pass = 0;
+    for (int64_t lo = 0; lo < nslots; lo += RB_PASS_SLOTS, ++pass) {
+        const int64_t m = std::min<int64_t>(RB_PASS_SLOTS, nslots - lo);
+        hipError_t e = records_bucket_pass(recs, rec_off, nstreams, m, cap, force_stable, seg_off, seg_len,
+                                           out_ns, counts, st, tiny, (uint32_t)lo, nslots, pass);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // Whole record-stream report statistics: bucketing (which reduces the staged buckets of <=

@@ -399,3 +399,58 @@ def test_records_stats_wide_keys(n):
             v = O.key_to_f32(O.duration_key(ns)).astype(np.float64) if s != 1 else ns.astype(np.float64)
             np.testing.assert_allclose(st.avg[g].item(), v.mean() / 1000, rtol=2.5e-7)
             np.testing.assert_allclose(st.std[g].item(), v.std() / 1000, rtol=1e-6)
+
+
+def test_profiler_more_kernels_than_one_bucketing_pass():
+    # the reference's per-kernel map is unbounded (CuptiProfiler.cpp:189-198);
+    # ~20,000 distinct composite keys in ONE report interval (past the 12,288 slots one bucketing
+    # pass counts in LDS) are bucketed in passes over slot ranges and reduced like any other
+    maxs = int(cupti.N.lib().nvrx_records_max_slots())
+    nk = maxs + 7_700
+    rng = np.random.default_rng(20_000)
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=16)
+    try:
+        p.initialize()
+        p.start()
+        names = [f"dyn_{i:06d}_blk_128_1_1_grid_{i % 31 + 1}_1_1" for i in range(nk)]
+        slots = np.array([p.register_kernel(n) for n in names], np.uint32)
+        cnt = rng.integers(1, 24, size=nk)                   # some rings overflow (cap 16)
+        sl = np.repeat(slots, cnt)
+        ns = rng.integers(1000, 3_000_000, size=sl.size, dtype=np.uint64)
+        order = rng.permutation(sl.size)
+        p.push_slots(sl[order], ns[order])
+        st = p.get_stats_columns()
+        assert len(st.names) == nk and st.names == sorted(names)
+        pos = {n: i for i, n in enumerate(st.names)}
+        for k in list(range(0, nk, 997)) + [maxs - 1, maxs, maxs + 1, nk - 1]:
+            d = ns[order][sl[order] == slots[k]]
+            r = _oracle_slot_stats(d, 16)
+            i = pos[names[k]]
+            got = (int(st.num[i]), np.float32(st.min[i]), np.float32(st.max[i]), np.float32(st.med[i]),
+                   np.float32(st.avg[i]), np.float32(st.std[i]))
+            assert got == r, names[k]
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("nslots,cap", [(30_000, 8192), (25_001, 3)])
+def test_records_stats_slot_tables_past_one_pass(nslots, cap):
+    # nvrx_records_stats / nvrx_records_bucket with more slots than one pass's LDS counters:
+    # three passes over slot ranges, every statistic against the oracle
+    rng = np.random.default_rng(nslots)
+    recs, off = _streams(rng, 3, nslots, 0, 4)
+    d_recs = torch.from_numpy(np.ascontiguousarray(recs).view(np.int32)).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    st = ops.records_stats(d_recs, d_off, nslots, cap, min(cap, 4), mode=ops.STATS_FAST).cpu()
+    ref = O.records_stats(recs, off, nslots, cap=cap, nthreads=4)
+    for f in ("num", "min", "max", "med", "avg", "std"):  # <= 4 records: bit-exact in every field
+        assert np.array_equal(getattr(st, f).numpy().view(np.int32), ref[f].view(np.int32)), f
+    seg_off, seg_len, out_ns, counts = (t.cpu().numpy() for t in ops.records_bucket(d_recs, d_off, nslots, cap))
+    for t in range(3):
+        stream = recs[off[t]:off[t + 1]]
+        for s in list(range(0, nslots, 1777)) + [12287, 12288, 24575, 24576, nslots - 1]:
+            pushed = stream[stream[:, 0] == s, 1]
+            g = t * nslots + s
+            assert counts[g] == pushed.size and seg_len[g] == min(pushed.size, cap)
+            got = out_ns[seg_off[g]:seg_off[g] + seg_len[g]].view(np.uint32)
+            assert np.array_equal(np.sort(got), np.sort(pushed[-cap:]))

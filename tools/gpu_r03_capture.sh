@@ -7,7 +7,7 @@ mkdir -p "$OUT"
 cd "$R"
 : > "$OUT/cost.jsonl"
 for rep in 1 2 3; do
-  for mode in none stopped started; do
+  for mode in none stopped started cycle; do
     timeout -k 5 60 ./tools/capture_cost $mode 20000 >> "$OUT/cost.jsonl" 2> "$OUT/err_$mode.log" || { echo "fail $mode"; tail -3 "$OUT/err_$mode.log"; exit 1; }
   done
 done
