@@ -4,6 +4,8 @@
 #pragma once
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "nvrx_common.h"
 #include "nvrx_internal.h"
 
@@ -137,6 +139,16 @@ __device__ __forceinline__ void write_empty(const nvrx_stats_soa& o, int64_t s) 
 //   sd = sum(d), sq = sum((d - c)^2) over the n samples, d = x - MIN.
 //   avg = (n MIN + sd) / (1000 n)               (numerator exact in f64)
 //   std = sqrtf(f32((n sq - (sd - n c)^2) / (1000 n)^2))  (population std, CuptiProfiler.cpp:66-70)
+// num / dd from the hardware reciprocal refined by two Newton steps and one residual
+// correction (~1e-16 relative; emit_stats and the group epilogue share it, so both round alike)
+__device__ __forceinline__ double quot_f64(double num, double dd) {
+    double rc = __builtin_amdgcn_rcp(dd);
+    rc = __builtin_fma(rc, __builtin_fma(-dd, rc, 1.0), rc);
+    rc = __builtin_fma(rc, __builtin_fma(-dd, rc, 1.0), rc);
+    double q = num * rc;
+    return __builtin_fma(__builtin_fma(-dd, q, num), rc, q);
+}
+
 __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, int n,
                                            unsigned mn, unsigned mx, unsigned d0, unsigned d1,
                                            double sd, double sq, unsigned c, const ColRef& cr) {
@@ -163,11 +175,7 @@ __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, i
     const double vq = __builtin_fma(sq, dn, -(se * se));
     const double num = lane == 0 ? __builtin_fma((double)mn, dn, sd) : (vq > 0.0 ? vq : 0.0);
     const double dd = lane == 0 ? den : den * den;
-    double rc = __builtin_amdgcn_rcp(dd);
-    rc = __builtin_fma(rc, __builtin_fma(-dd, rc, 1.0), rc);
-    rc = __builtin_fma(rc, __builtin_fma(-dd, rc, 1.0), rc);
-    double q = num * rc;
-    q = __builtin_fma(__builtin_fma(-dd, q, num), rc, q);
+    const double q = quot_f64(num, dd);
     const float r = lane == 0 ? (float)q : __builtin_amdgcn_sqrtf((float)q);
     const float avg = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 0));
     const float sdv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r), 1));
@@ -180,6 +188,27 @@ __device__ __forceinline__ void emit_stats(const nvrx_stats_soa& o, int64_t s, i
         o.std[s] = sdv;
         cr.add(s, med);
     }
+}
+
+// emit_stats for one segment per lane (the group epilogues: lane j holds segment s0 + j's
+// results); the same arithmetic, so the same bits.  k0 / k1: the middle-rank keys (mn + d0,
+// mn + d1).
+__device__ __forceinline__ void emit_lane(const nvrx_stats_soa& o, int64_t s, int n, unsigned mn,
+                                          unsigned mx, unsigned k0, unsigned k1, double sd,
+                                          double sq, unsigned c, const ColRef& cr) {
+    const float f0 = ns_to_us(k0), f1 = ns_to_us(k1);
+    const float med = (n & 1) ? f0 : (f0 + f1) / 2;  // CuptiProfiler.cpp:58
+    const double dn = (double)n;
+    const double se = sd - dn * (double)c;
+    const double den = 1000.0 * dn;
+    const double vq = __builtin_fma(sq, dn, -(se * se));
+    o.num[s] = n;
+    o.min[s] = ns_to_us(mn);
+    o.max[s] = ns_to_us(mx);
+    o.med[s] = med;
+    o.avg[s] = (float)quot_f64(__builtin_fma((double)mn, dn, sd), den);
+    o.std[s] = __builtin_amdgcn_sqrtf((float)quot_f64(vq > 0.0 ? vq : 0.0, den * den));
+    cr.add(s, med);
 }
 
 // FAST AVG / STD of a segment whose keys reach NVRX_KEY_WIDE (a kernel of 3.76 s or more): the
@@ -286,10 +315,14 @@ struct OccV {  // the masked PL=128 variant gets the whole 256-register budget
 // vectors; element i of the wave holds sample e = (j*64 + lane)*4 + t - m0, i = 4j + t).
 // FULL: every slot is a sample (m0 = 0, n = 64*PL).  !FULL: slots outside [0, n) were
 // set to x0 (a sample) by the caller.
+struct FastOut {
+    unsigned mn, mx, d0, d1, c;  // d0 / d1: the two middle ranks, relative to mn
+    double sd, sq;
+};
+
 template <int PL, bool FULL>
-__device__ __forceinline__ unsigned fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
-                                          int64_t s, unsigned* hist, const nvrx_stats_soa& out,
-                                          const ColRef& cr) {
+__device__ __forceinline__ FastOut fast_core(unsigned (&v)[PL], int n, int m0, unsigned x0,
+                                             unsigned* hist) {
     constexpr int NB = Bins<PL>::NB;
     constexpr int LOGNB = Bins<PL>::LOG;
     constexpr int BPL = Bins<PL>::BPL;
@@ -460,9 +493,16 @@ __device__ __forceinline__ unsigned fast_body(unsigned (&v)[PL], int n, int m0, 
         wlo += b0 << shift;
         shift = shift > LOGNB ? shift - LOGNB : 0;
     }
+    return FastOut{mn, mx, d0, d1, c, sd, sq};
+}
 
-    emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
-    return mx;
+template <int PL, bool FULL>
+__device__ __forceinline__ unsigned fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
+                                          int64_t s, unsigned* hist, const nvrx_stats_soa& out,
+                                          const ColRef& cr) {
+    const FastOut r = fast_core<PL, FULL>(v, n, m0, x0, hist);
+    emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, r.sd, r.sq, r.c, cr);
+    return r.mx;
 }
 
 // Lean body for FULL segments (n = 64*PL, every slot a sample) -- the C2/C3 matrix path,
@@ -479,9 +519,19 @@ __device__ __forceinline__ unsigned fast_body(unsigned (&v)[PL], int n, int m0, 
 //     d - hi is the largest sample below hi (likewise the min of d - lo), for any range.
 // The wave reductions finish with row_bcast (wave_*_b).
 template <int PL>
-__device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
-                                          unsigned* hist, const nvrx_stats_soa& out,
-                                          const ColRef& cr) {
+struct LeanOut {
+    // the exact sum of d: an integer for PL <= 16 (the group kernel's epilogue takes it from
+    // scalar registers), its (exact) f64 value above
+    using Sd = typename std::conditional<(PL <= 16), uint64_t, double>::type;
+    unsigned mn, mx, d0, d1, c;  // d0 / d1: the two middle ranks, relative to mn
+    Sd sd;
+    double sq;
+};
+
+template <int PL>
+__device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsigned x0,
+                                                 unsigned* hist) {
+    using Sd = typename LeanOut<PL>::Sd;
     constexpr int NB = Bins<PL>::NB;
     constexpr int LOGNB = Bins<PL>::LOG;
     constexpr int BPL = Bins<PL>::BPL;
@@ -496,28 +546,56 @@ __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned
     const unsigned mn = wave_min_b(lmn);
     const unsigned mx = wave_max_b(lmx);
     const unsigned range = mx - mn;
+    // Segments spanning < 2^23 ns (every configs[] shape) hold x = d + B, B = 0x4B000000 = the
+    // f32 bits of 2^23: x is then the bit pattern of the float 2^23 + d, so the squares take
+    // the registers as they are (no int -> float conversion per sample).  Selection is
+    // translation invariant -- the histogram takes bits [shift, shift + LOGNB) of x (those of
+    // d: bits(range) <= 23), the walk starts at wlo = B -- and B leaves the results at the end.
+    const unsigned B = range < (1u << 23) ? 0x4B000000u : 0u;
+    const unsigned off = B - mn;
 #pragma unroll
-    for (int i = 0; i < PL; ++i) v[i] -= mn;
+    for (int i = 0; i < PL; ++i) v[i] += off;
 
     // ---- exact sum + squares about the pivot c (lane_sums order: pairs, groups of 16) ----
     unsigned c = x0 - mn;
-    double sd, acc;
+    Sd sd;
+    double acc;
     if (range < (1u << 24)) {
         constexpr int G = PL < 16 ? PL : 16;
         unsigned ls = 0;
         acc = 0.0;
-        const f32x2 cc = {(float)c, (float)c};
+        if (B) {
+            // (2^23 + d) - (2^23 + c): both exact in f32, and so is the difference
+            const float fc = __builtin_bit_cast(float, B + c);
+            const f32x2 cc = {fc, fc};
 #pragma unroll
-        for (int g = 0; g < PL; g += G) {
-            f32x2 q = {0.0f, 0.0f};
+            for (int g = 0; g < PL; g += G) {
+                f32x2 q = {0.0f, 0.0f};
 #pragma unroll
-            for (int i = 0; i < G; i += 2) {
-                ls += v[g + i];
-                ls += v[g + i + 1];
-                const f32x2 e = (f32x2){(float)v[g + i], (float)v[g + i + 1]} - cc;
-                q = __builtin_elementwise_fma(e, e, q);
+                for (int i = 0; i < G; i += 2) {
+                    ls += v[g + i];
+                    ls += v[g + i + 1];
+                    const f32x2 e = (f32x2){__builtin_bit_cast(float, v[g + i]),
+                                            __builtin_bit_cast(float, v[g + i + 1])} - cc;
+                    q = __builtin_elementwise_fma(e, e, q);
+                }
+                acc += (double)q.x + (double)q.y;
             }
-            acc += (double)q.x + (double)q.y;
+            ls -= (unsigned)PL * B;  // sum d mod 2^32, exact: PL * 2^23 < 2^32
+        } else {
+            const f32x2 cc = {(float)c, (float)c};
+#pragma unroll
+            for (int g = 0; g < PL; g += G) {
+                f32x2 q = {0.0f, 0.0f};
+#pragma unroll
+                for (int i = 0; i < G; i += 2) {
+                    ls += v[g + i];
+                    ls += v[g + i + 1];
+                    const f32x2 e = (f32x2){(float)v[g + i], (float)v[g + i + 1]} - cc;
+                    q = __builtin_elementwise_fma(e, e, q);
+                }
+                acc += (double)q.x + (double)q.y;
+            }
         }
         if (PL <= 16) {
             // integer reduction: a row of 16 lanes sums to < 16 * 16 * 2^24 = 2^32 (no
@@ -527,9 +605,9 @@ __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned
             r += dpp<0x4E>(r);
             r += dpp<0x141>(r);
             r += dpp<0x140>(r);
-            sd = (double)(((uint64_t)rl(r, 0) + rl(r, 16)) + ((uint64_t)rl(r, 32) + rl(r, 48)));
+            sd = (Sd)(((uint64_t)rl(r, 0) + rl(r, 16)) + ((uint64_t)rl(r, 32) + rl(r, 48)));
         } else {
-            sd = wave_sum_f64_b((double)ls);
+            sd = (Sd)wave_sum_f64_b((double)ls);
         }
     } else {  // rare: a ring spanning >= 16.7 ms -- fast_body's sums
         uint64_t sdi;
@@ -539,7 +617,7 @@ __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned
             c = 0u;
             lane_sums_f64<PL>(v, sdi, acc);
         }
-        sd = wave_sum_f64_b((double)sdi);
+        sd = (Sd)wave_sum_f64_b((double)sdi);
     }
     const double sq = wave_sum_f64_b(acc);
 
@@ -556,7 +634,7 @@ __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
-        const unsigned h = v[i] >> shift;
+        const unsigned h = __builtin_amdgcn_ubfe(v[i], (unsigned)shift, (unsigned)LOGNB);  // d >> shift
         if (KEEPBIN) hb[KEEPBIN ? i : 0] = h;
         atomicAdd(&hist[h], 1u);
     }
@@ -564,7 +642,7 @@ __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned
 
     const unsigned t0 = (unsigned)((n & 1) ? n / 2 : n / 2 - 1);
     const unsigned t1 = (unsigned)(n / 2);
-    unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
+    unsigned wlo = B, below = 0, d0 = 0, d1 = 0;
     for (int level = 0;; ++level) {
         if (level > 0) {
 #pragma unroll
@@ -656,8 +734,16 @@ __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned
         wlo += b0 << shift;
         shift = shift > LOGNB ? shift - LOGNB : 0;
     }
-    emit_stats(out, s, n, mn, mx, d0, d1, sd, sq, c, cr);
-    return mx;
+    return LeanOut<PL>{mn, mx, d0 - B, d1 - B, c, sd, sq};
+}
+
+template <int PL>
+__device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
+                                          unsigned* hist, const nvrx_stats_soa& out,
+                                          const ColRef& cr) {
+    const LeanOut<PL> r = lean_core<PL>(v, n, x0, hist);
+    emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, (double)r.sd, r.sq, r.c, cr);
+    return r.mx;
 }
 
 // HBM -> VGPR in two steps, so a caller can issue the next segment's loads before it
@@ -764,6 +850,61 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     unsigned x0;
     load_segment<PL, true>(p, n, v, m0, x0);
     if (lean_body<PL>(v, n, x0, s, hist, out, cr) >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
+}
+
+// FULL segments of <= 1024 samples (the configs[2] shape), where the statistics are bound by
+// VALU issue: each wave reduces `group` consecutive segments one after another and keeps what
+// lean_core returns for segment s0 + j in lane j (one compare and nine selects), so the epilogue -- the
+// unit conversions, the f64 quotients and the root, the stores -- runs once per group,
+// lane-parallel with coalesced stores, instead of once per segment on one busy lane (~55 VALU,
+// half of them f64).  Same arithmetic as emit_stats, so the same bits.
+template <int PL, class Segs>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
+void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, nvrx_stats_soa out, ColRef cr) {
+    static_assert(PL <= 16, "integer sums (LeanOut::Sd) only for PL <= 16");
+    constexpr int NB = Bins<PL>::NB;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id();
+    const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * group;
+    if (s0 >= nseg) return;
+    const int cnt = (int)(nseg - s0 < group ? nseg - s0 : group);
+    unsigned* hist = lds_hist + wave * NB;
+    unsigned a_mn = 0, a_mx = 0, a_k0 = 0, a_k1 = 0, a_c = 0, a_sdlo = 0, a_sdhi = 0, a_sqlo = 0, a_sqhi = 0;
+    uint64_t wide = 0;
+    int n = 0;
+    for (int j = 0; j < cnt; ++j) {
+        const uint32_t* p;
+        segs.get(s0 + j, p, n);
+        unsigned v[PL];
+        int m0;
+        unsigned x0;
+        load_segment<PL, true>(p, n, v, m0, x0);
+        const LeanOut<PL> r = lean_core<PL>(v, n, x0, hist);
+        const uint64_t sqb = (uint64_t)__double_as_longlong(r.sq);
+        const bool mine = lane == j;  // one compare, nine selects
+        a_mn = mine ? r.mn : a_mn;
+        a_mx = mine ? r.mx : a_mx;
+        a_k0 = mine ? r.mn + r.d0 : a_k0;
+        a_k1 = mine ? r.mn + r.d1 : a_k1;
+        a_c = mine ? r.c : a_c;
+        a_sdlo = mine ? (uint32_t)r.sd : a_sdlo;
+        a_sdhi = mine ? (uint32_t)(r.sd >> 32) : a_sdhi;
+        a_sqlo = mine ? (uint32_t)sqb : a_sqlo;
+        a_sqhi = mine ? (uint32_t)(sqb >> 32) : a_sqhi;
+        if (r.mx >= NVRX_KEY_WIDE) wide |= 1ull << j;
+    }
+    if (lane < cnt)
+        emit_lane(out, s0 + lane, n, a_mn, a_mx, a_k0, a_k1,
+                  (double)(((uint64_t)a_sdhi << 32) | a_sdlo),
+                  __longlong_as_double((long long)(((uint64_t)a_sqhi << 32) | a_sqlo)), a_c, cr);
+    while (wide) {  // keys of >= 3.76 s: the decoded moments (rare)
+        const int j = __builtin_ffsll(wide) - 1;
+        wide &= wide - 1;
+        const uint32_t* p;
+        segs.get(s0 + j, p, n);
+        wide_moments(p, n, s0 + j, out);
+    }
 }
 
 // Batcher's odd-even merge sort over N registers (N a power of two) as a compile-time list of
@@ -982,11 +1123,26 @@ static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream
     return hipGetLastError();
 }
 
+// segments per wave of the group kernel: up to 64 while the grid keeps >= 32768 waves
+static inline int lean_group(int64_t nseg) {
+    const int64_t g = nseg / 32768;
+    return g < 1 ? 1 : g > 64 ? 64 : (int)g;
+}
+
 template <int PL, class Segs>
 static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
                       const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
     // lean_body: bit-identical to fast_body<PL, true>, 6-9 % faster (tools/mb_c3.hip)
+    if constexpr (PL <= 16) {
+        if (full) {
+            const int g = lean_group(nseg);
+            const int64_t waves = (nseg + g - 1) / g;
+            hipLaunchKernelGGL((seg_stats_lean_group_kernel<PL, Segs>), dim3((unsigned)((waves + 3) / 4)),
+                               block, 0, st, segs, nseg, g, out, cr);
+            return;
+        }
+    }
     if (full)
         hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else

@@ -202,8 +202,12 @@ struct ListPrefetch {
     static constexpr bool on = PL <= 16;
 };
 template <int PL>
-struct ListOcc {  // the prefetch buffer costs PL more VGPRs
-    static constexpr int W = PL == 16 ? 6 : OccV<PL, false>::W;
+struct ListGroup {  // one epilogue per chunk (emit_lane): the short classes, whose chunks are long
+    static constexpr bool on = PL <= 8;
+};
+template <int PL>
+struct ListOcc {  // the prefetch buffer costs PL more VGPRs, the chunk's results nine
+    static constexpr int W = PL == 16 ? 6 : PL == 8 ? 7 : OccV<PL, false>::W;
 };
 constexpr int LIST_CHUNK = 16;
 
@@ -241,6 +245,26 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
         const uint32_t* p;
         int n;
         desc(0, s, p, n);
+        // the chunk's results, segment j in lane j (lane j already holds its id and length):
+        // one epilogue per chunk, lane-parallel (emit_lane), instead of one per segment
+        unsigned a_mn = 0, a_mx = 0, a_k0 = 0, a_k1 = 0, a_c = 0, a_sdlo = 0, a_sdhi = 0, a_sqlo = 0,
+                 a_sqhi = 0;
+        uint32_t wide = 0;
+        const auto keep = [&](int j, const FastOut& r) {
+            const uint64_t sdb = (uint64_t)__double_as_longlong(r.sd);
+            const uint64_t sqb = (uint64_t)__double_as_longlong(r.sq);
+            const bool mine = lane == j;
+            a_mn = mine ? r.mn : a_mn;
+            a_mx = mine ? r.mx : a_mx;
+            a_k0 = mine ? r.mn + r.d0 : a_k0;
+            a_k1 = mine ? r.mn + r.d1 : a_k1;
+            a_c = mine ? r.c : a_c;
+            a_sdlo = mine ? (uint32_t)sdb : a_sdlo;
+            a_sdhi = mine ? (uint32_t)(sdb >> 32) : a_sdhi;
+            a_sqlo = mine ? (uint32_t)sqb : a_sqlo;
+            a_sqhi = mine ? (uint32_t)(sqb >> 32) : a_sqhi;
+            if (r.mx >= NVRX_KEY_WIDE) wide |= 1u << j;
+        };
         unsigned v[PL];
         if (ListPrefetch<PL>::on) {
             issue_loads<PL>(p, n, v);
@@ -256,7 +280,9 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
                 int m0;
                 unsigned x0;
                 finish_loads<PL, false>(p, n, v, m0, x0);
-                if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
+                if (ListGroup<PL>::on)
+                    keep(j, fast_core<PL, false>(v, n, m0, x0, hist));
+                else if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
                     wide_moments(p, n, s, out);
 #pragma unroll
                 for (int i = 0; i < PL; ++i) v[i] = w[i];
@@ -270,9 +296,21 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
                 int m0;
                 unsigned x0;
                 load_segment<PL, false>(p, n, v, m0, x0);
-                if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
+                if (ListGroup<PL>::on)
+                    keep(j, fast_core<PL, false>(v, n, m0, x0, hist));
+                else if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
                     wide_moments(p, n, s, out);
             }
+        }
+        if (ListGroup<PL>::on && lane < m)
+            emit_lane(out, (int64_t)sid, nn, a_mn, a_mx, a_k0, a_k1,
+                      __longlong_as_double((long long)(((uint64_t)a_sdhi << 32) | a_sdlo)),
+                      __longlong_as_double((long long)(((uint64_t)a_sqhi << 32) | a_sqlo)), a_c, cr);
+        while (wide) {  // keys of >= 3.76 s: the decoded moments (rare)
+            const int j = __builtin_ffs(wide) - 1;
+            wide &= wide - 1;
+            desc(j, s, p, n);
+            wide_moments(p, n, s, out);
         }
     }
 }

@@ -340,3 +340,40 @@ def test_ragged_class_boundaries(mode, aligned16):
             v = key_values(host[off[s]:off[s + 1]])
             assert abs(got[3] - v.mean() / 1000) <= 2.5e-7 * v.mean() / 1000 or got[3] == want[3], (s, L)
             assert abs(got[4] - v.std() / 1000) <= 1e-6 * v.std() / 1000 + 1e-6 or got[4] == want[4], (s, L)
+
+
+@pytest.mark.parametrize("n", [256, 512, 1024])
+def test_grouped_full_segments(n):
+    """Full segments of <= 1024 samples run the group kernel (several segments per wave, the
+    epilogue once per group, lane-parallel): enough segments for groups of > 1 (nseg / 32768),
+    a partial last group, the edge distributions (full 32-bit range = wide keys, clusters,
+    zeros) at the first, last and middle positions of groups, and the fused column reference."""
+    rng = np.random.default_rng(n)
+    K = 37
+    nseg = K * (3550 if n == 1024 else 3601)
+    group = min(64, max(1, nseg // 32768))
+    assert group > 1 and nseg % group  # groups of 4 and a partial last group
+    host = rng.integers(2000, 2_200_000, size=nseg * n, dtype=np.uint32)
+    edges = _edge_segments(n)
+    where = [0, group - 1, group, 5 * group + group // 2, nseg - 1, nseg - group, 3 * group - 1,
+             nseg // 2, 7 * group + 1, 11 * group - 1]
+    for w, seg in zip(where, edges):
+        host[w * n:(w + 1) * n] = seg
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    col = torch.empty(2 * K, dtype=torch.int32, device=DEV)
+    st = ops.segment_stats_strided(ns, nseg, n, 0, n, cap=0, mode=ops.STATS_FAST, col_ref=col, ncols=K)
+    ref = _oracle_segments(host, nseg, n, 0, n, 0)
+    _check(st, ref)
+    # FAST AVG / STD against the exact moments (vectorised: segments of the random bulk are
+    # below the wide-key threshold; the edge segments take key_values)
+    g = st.cpu()
+    x = host.reshape(nseg, n).astype(np.float64)
+    avg, std = x.mean(axis=1) / 1000.0, x.std(axis=1) / 1000.0
+    for w in where:
+        v = key_values(host[w * n:(w + 1) * n])
+        avg[w], std[w] = v.mean() / 1000.0, v.std() / 1000.0
+    np.testing.assert_allclose(g.avg.numpy(), avg, rtol=2.5e-7, atol=1e-30)
+    np.testing.assert_allclose(g.std.numpy(), std, rtol=1e-6, atol=1e-6 * avg.max())
+    want = O.kernel_ref(ref["num"].reshape(-1, K), ref["med"].reshape(-1, K))
+    got = col.cpu().numpy()
+    assert np.array_equal(got[:K].view(np.float32), want) and not got[K:].any()

@@ -5,7 +5,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"))
+# AB_PKG: package root to import (a saved copy with another libnvrx_hip.so, e.g. tools/ab_pkg)
+sys.path.insert(0, os.environ.get("AB_PKG", os.path.join(ROOT, "nvidia-resiliency-ext-x_amd")))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -34,5 +35,5 @@ for _ in range(n):
 if os.environ.get("AB_DUMP"):
     torch.save({f: getattr(ref, f) for f in ("num", "min", "max", "med", "avg", "std")}, os.environ["AB_DUMP"])
 env = {k: v for k, v in os.environ.items() if k.startswith("NVRX_")}
-print(f"R={R} records={R*N} records_stats_ms={ts/n:.3f} "
+print(f"pkg={os.environ.get('AB_PKG', 'tree')} R={R} records={R*N} records_stats_ms={ts/n:.3f} "
       f"({R*N*8/(ts/n)/1e6:.0f} GB/s at 8 B/rec) env={env}")
