@@ -1,4 +1,5 @@
-"""Interleaved A/B of the configs[2] (4096 x 2048 x 1024) statistics kernel: argv[1] = package
+"""Interleaved A/B of the configs[2] (4096 x 2048 x 1024; AB_R / AB_S: another shape, e.g.
+configs[1] = 64 / 10000) statistics kernel: argv[1] = package
 root to import (the current tree or a saved copy with another libnvrx_hip.so), argv[2] = reps.
 Prints ms per launch."""
 import os
@@ -9,7 +10,7 @@ import torch  # noqa: E402
 
 from nvidia_resiliency_ext.straggler import ops, synth  # noqa: E402
 
-R, K, S, CAP = 4096, 2048, 1024, 8192
+R, K, S, CAP = int(os.environ.get("AB_R", 4096)), 2048, int(os.environ.get("AB_S", 1024)), 8192
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 ns = synth.synth_matrix(R, K, S, device="cuda")
 out = ops.SegmentStats.empty(R * K, "cuda")

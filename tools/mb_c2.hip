@@ -116,6 +116,55 @@ void row_split(const uint32_t* ns, unsigned* out) {
     if (m == 0x12345678u) out[g] = m;
 }
 
+// (g) 4 waves per row (PLW = 32) plus ITER x 32 dependent VALU per wave after the loads (a
+//     stand-in for the statistics), one row per workgroup or (PREF) a persistent workgroup over
+//     rows with the next row's loads issued before the current row's "reduction"
+template <int ITER, bool PREF, int W>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W)))
+void row_compute(const uint32_t* ns, unsigned* out, int64_t rows_per_block) {
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    auto load = [&](int64_t row, unsigned (&v)[32]) {
+        const uint32_t* p = ns + row * STRIDE1 + BEGIN1 + wave * 2048;
+        const uintptr_t pa = (uintptr_t)p;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)pa);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(pa >> 32));
+        const auto r = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 8192, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16, j * 1024, 2);
+            v[4 * j] = q.x, v[4 * j + 1] = q.y, v[4 * j + 2] = q.z, v[4 * j + 3] = q.w;
+        }
+    };
+    auto work = [&](const unsigned (&v)[32]) {
+        float x = (float)lane;
+        for (int k = 0; k < ITER; ++k) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) x = __builtin_fmaf(x, 0.999f, __builtin_bit_cast(float, v[i] & 0x3FFFFFFFu));
+        }
+        return x;
+    };
+    float acc = 0.0f;
+    unsigned v[32];
+    if (PREF) {
+        load(r0, v);
+        for (int64_t j = 0; j < rows_per_block && r0 + j < ROWS1; ++j) {
+            unsigned w[32];
+            load(r0 + j + 1 < ROWS1 && j + 1 < rows_per_block ? r0 + j + 1 : r0 + j, w);
+            acc += work(v);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) v[i] = w[i];
+        }
+    } else {
+        for (int64_t j = 0; j < rows_per_block && r0 + j < ROWS1; ++j) {
+            load(r0 + j, v);
+            acc += work(v);
+        }
+    }
+    if (acc == 1.2345f) out[blockIdx.x] = 1;
+}
+
 int main() {
     const size_t bytes = (size_t)NSEG * LEN * 4;
     uint32_t* ns;
@@ -169,6 +218,21 @@ int main() {
         time1("row P=2 W4", [&] { row_split<2, 4><<<ROWS1 * 2 / 4, 256>>>(ns, out); });
         time1("row P=4 W8", [&] { row_split<4, 8><<<ROWS1 * 4 / 4, 256>>>(ns, out); });
         time1("row P=8 W8", [&] { row_split<8, 8><<<ROWS1 * 8 / 4, 256>>>(ns, out); });
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+        time1("P4 work0", [&] { row_compute<0, false, 8><<<ROWS1, 256>>>(ns, out, 1); });
+        time1("P4 work8", [&] { row_compute<8, false, 8><<<ROWS1, 256>>>(ns, out, 1); });
+        time1("P4 work16", [&] { row_compute<16, false, 8><<<ROWS1, 256>>>(ns, out, 1); });
+        time1("P4 work32", [&] { row_compute<32, false, 8><<<ROWS1, 256>>>(ns, out, 1); });
+        for (int rpb : {4, 16}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "P4 work8 pref rpb%d W6", rpb);
+            time1(nm, [&] { row_compute<8, true, 6><<<ROWS1 / rpb, 256>>>(ns, out, rpb); });
+            snprintf(nm, sizeof nm, "P4 work16 pref rpb%d W6", rpb);
+            time1(nm, [&] { row_compute<16, true, 6><<<ROWS1 / rpb, 256>>>(ns, out, rpb); });
+            snprintf(nm, sizeof nm, "P4 work16 seq rpb%d W8", rpb);
+            time1(nm, [&] { row_compute<16, false, 8><<<ROWS1 / rpb, 256>>>(ns, out, rpb); });
+        }
     }
     CK(hipDeviceSynchronize());
     return 0;
