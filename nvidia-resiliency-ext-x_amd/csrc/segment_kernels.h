@@ -311,206 +311,14 @@ struct OccV {  // the masked PL=128 variant gets the whole 256-register budget
 #define NVRX_LOAD_AUX 2  // nt: measured +1.5-2% on C2/C3 over the default policy
 #endif
 
-// Reduce one segment held in registers (v: 64*PL slots, lane-interleaved in 16-B
-// vectors; element i of the wave holds sample e = (j*64 + lane)*4 + t - m0, i = 4j + t).
-// FULL: every slot is a sample (m0 = 0, n = 64*PL).  !FULL: slots outside [0, n) were
-// set to x0 (a sample) by the caller.
-struct FastOut {
-    unsigned mn, mx, d0, d1, c;  // d0 / d1: the two middle ranks, relative to mn
-    double sd, sq;
-};
-
-template <int PL, bool FULL>
-__device__ __forceinline__ FastOut fast_core(unsigned (&v)[PL], int n, int m0, unsigned x0,
-                                             unsigned* hist) {
-    constexpr int NB = Bins<PL>::NB;
-    constexpr int LOGNB = Bins<PL>::LOG;
-    constexpr int BPL = Bins<PL>::BPL;
-    const int lane = lane_id();
-    const int pad = FULL ? 0 : 64 * PL - n;  // padding elements (not samples of the segment)
-
-    // ---- pass A1: MIN / MAX ----
-    unsigned lmn = v[0], lmx = v[0];
-#pragma unroll
-    for (int i = 1; i < PL; ++i) {
-        lmn = min(lmn, v[i]);
-        lmx = max(lmx, v[i]);
-    }
-    const unsigned mn = wave_min_u32(lmn);
-    const unsigned mx = wave_max_u32(lmx);
-
-    // From here on v holds d = x - MIN (in place: one register per sample).
-    // Padding := d 0 (= MIN): contributes 0 to the sums below and occupies the lowest
-    // `pad` ranks, so the median ranks simply shift by `pad`.
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-        if (FULL) {
-            v[i] -= mn;
-        } else {
-            const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
-            v[i] = (e < (unsigned)n) ? v[i] - mn : 0u;
-        }
-    }
-
-    const unsigned range = mx - mn;
-    const int bits = 32 - __clz((int)range);  // 0 when range == 0
-    int shift = bits > LOGNB ? bits - LOGNB : 0;
-
-    // ---- pass A2: exact sums + first histogram level ----
-    // pivot c: the segment's first sample, when every d - c fits an int (FULL segments
-    // spanning < 2^31 ns); otherwise c = 0 with f64 squares (padding holds d = 0)
-    const bool pivot = FULL && range < 0x80000000u;
-    const unsigned c = pivot ? x0 - mn : 0u;
-    uint64_t sdl;
-    double sql;
-    if (pivot)
-        lane_sums<PL>(v, c, sdl, sql);
-    else
-        lane_sums_f64<PL>(v, sdl, sql);
-    const double sd = wave_sum_f64((double)sdl);  // exact: integer-valued, < 2^53
-    const double sq = wave_sum_f64(sql);
-    // PADSKIP: the padding (d = 0, bin 0 at every level whose window starts at 0) is counted
-    // by the bin's initial value instead of one atomic per padding slot -- those atomics all
-    // hit one LDS word, a same-address serialisation.  Lane L's register i holds slot
-    // e = 256 (i >> 2) + (i & 3) + 4 L - m0.  Measured on configs[3]'s ragged classes
-    // (tools/gpu_ab_padskip.sh): PL 16 / 32 / 64 -12 / -25 / -16 %; PL 4 / 8 +3 % (little
-    // padding contention to remove), PL 128 +25 % (register pressure): kept for 16..64.
-    constexpr bool PADSKIP = !FULL && PL >= 16 && PL <= 64;
-    const unsigned pad_bin0 = PADSKIP ? (unsigned)pad : 0u;
-    const int eb = 4 * lane - m0;
-    const auto real = [&](int i) {
-        return !PADSKIP || (unsigned)(eb + 256 * (i >> 2) + (i & 3)) < (unsigned)n;
-    };
-    // level-0 bins kept in registers for short segments (see lean_body; PL = 16 would spill
-    // the list kernel's prefetch registers)
-    constexpr bool KEEPBIN = PL <= 8;
-    unsigned hb[KEEPBIN ? PL : 1];
-#pragma unroll
-    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = (lane == 0 && j == 0) ? pad_bin0 : 0u;
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-        const unsigned h = v[i] >> shift;
-        if (KEEPBIN) hb[KEEPBIN ? i : 0] = h;
-        if (real(i)) atomicAdd(&hist[h], 1u);
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- median: radix select on d = x - MIN ----
-    // sorted real samples s[0..n); median = odd ? s[n/2] : (s[n/2-1] + s[n/2]) / 2
-    const unsigned t0 = (unsigned)(pad + ((n & 1) ? n / 2 : n / 2 - 1));
-    const unsigned t1 = (unsigned)(pad + n / 2);
-    unsigned wlo = 0, below = 0, d0 = 0, d1 = 0;
-    for (int level = 0;; ++level) {
-        if (level > 0) {
-            const unsigned pad0 = wlo == 0 ? pad_bin0 : 0u;
-#pragma unroll
-            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = (lane == 0 && j == 0) ? pad0 : 0u;
-            __builtin_amdgcn_wave_barrier();
-            const unsigned span = (unsigned)NB << shift;  // level > 0: fits in 32 bits
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const unsigned q = v[i] - wlo;  // wraps for d < wlo
-                if (q < span && real(i)) atomicAdd(&hist[q >> shift], 1u);
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        unsigned b0, c0, n0, b1;  // t1 is t0 or t0 + 1: located only past t0's bucket
-        hist_locate1<PL>(hist, t0 - below, b0, c0, n0);
-        if (t1 - below < c0 + n0) {
-            b1 = b0;
-        } else {
-            unsigned c1, n1;
-            hist_locate1<PL>(hist, t1 - below, b1, c1, n1);
-        }
-        if (b0 != b1) {
-            // s[t0] is the largest sample of bucket b0, s[t1] the smallest of bucket b1
-            unsigned lmax = 0, lmin = 0xFFFFFFFFu;
-            const unsigned lo0 = wlo + (b0 << shift), lo1 = wlo + (b1 << shift);
-            const unsigned width = 1u << shift;
-#pragma unroll
-            for (int i = 0; i < PL; ++i) {
-                const unsigned d = v[i];
-                if (d - lo0 < width) lmax = max(lmax, d);
-                if (d - lo1 < width) lmin = min(lmin, d);
-            }
-            d0 = wave_max_u32(lmax);
-            d1 = wave_min_u32(lmin);
-            break;
-        }
-        if (shift == 0) {
-            d0 = d1 = wlo + b0;
-            break;
-        }
-        if (n0 <= 64u) {
-            // compact the <= 64 candidates of bucket b0 into LDS (the histogram is consumed)
-            __builtin_amdgcn_wave_barrier();
-            unsigned base = 0;
-            const unsigned lo0 = wlo + (b0 << shift);
-            const unsigned width = 1u << shift;
-            if (KEEPBIN && level == 0) {
-#pragma unroll
-                for (int i = 0; i < PL; ++i) {
-                    const bool in = hb[KEEPBIN ? i : 0] == b0;
-                    const uint64_t bm = __ballot(in);
-                    if (in) hist[base + mbcnt(bm)] = v[i];
-                    base += (unsigned)__popcll(bm);
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < PL; ++i) {
-                    const unsigned d = v[i];
-                    const bool in = d - lo0 < width;
-                    const uint64_t bm = __ballot(in);
-                    if (in) hist[base + mbcnt(bm)] = d;
-                    base += (unsigned)__popcll(bm);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            const unsigned ci = (lane < (int)n0) ? hist[lane] : 0xFFFFFFFFu;
-            unsigned rank = 0;
-            if (shift <= 26) {  // one-compare unique keys, as in lean_body
-                const unsigned key = (lane < (int)n0) ? ((ci - lo0) << 6) | (unsigned)lane : 0xFFFFFFFFu;
-                for (int j = 0; j < (int)n0; j += 4) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) rank += (rl(key, j + u) < key) ? 1u : 0u;
-                }
-            } else {
-                for (int j = 0; j < (int)n0; ++j) {
-                    const unsigned cj = __builtin_amdgcn_readlane(ci, j);
-                    rank += (cj < ci || (cj == ci && j < lane)) ? 1u : 0u;
-                }
-            }
-            const unsigned r0 = t0 - below - c0, r1 = t1 - below - c0;
-            const int L0 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r0)) - 1;
-            const int L1 = __builtin_ffsll(__ballot(lane < (int)n0 && rank == r1)) - 1;
-            d0 = __builtin_amdgcn_readlane(ci, L0);
-            d1 = __builtin_amdgcn_readlane(ci, L1);
-            break;
-        }
-        // descend one level into bucket b0
-        below += c0;
-        wlo += b0 << shift;
-        shift = shift > LOGNB ? shift - LOGNB : 0;
-    }
-    return FastOut{mn, mx, d0, d1, c, sd, sq};
-}
-
-template <int PL, bool FULL>
-__device__ __forceinline__ unsigned fast_body(unsigned (&v)[PL], int n, int m0, unsigned x0,
-                                          int64_t s, unsigned* hist, const nvrx_stats_soa& out,
-                                          const ColRef& cr) {
-    const FastOut r = fast_core<PL, FULL>(v, n, m0, x0, hist);
-    emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, r.sd, r.sq, r.c, cr);
-    return r.mx;
-}
-
-// Lean body for FULL segments (n = 64*PL, every slot a sample) -- the C2/C3 matrix path,
-// where the kernel is VALU-bound for short segments (S = 1024: 523 VALU per wave with
-// fast_body, 465 here, SQ_INSTS_VALU).  Same results, bit for bit, as fast_body: the same
-// per-lane summation order, and wave reductions paired commutatively alike.  Per sample:
+// One wave per segment held in registers (v: 64*PL slots, lane-interleaved in 16-B vectors;
+// register i of lane L holds slot e = 256 (i >> 2) + 4 L + (i & 3) - m0).  MIN / MAX by wave
+// reductions; d = x - MIN in place; exact sums; MED by radix select on d with a wave-private LDS
+// histogram, the median's bucket resolved by candidate compaction and rank-by-compare, or by
+// the wrapped extremes of two buckets, or by another level.  Round 3 replaced the masked
+// (!FULL) body (fast_body: per-slot masks, f64 squares about 0) with this one.  Per sample:
 //   * the exact sum is one 32-bit add when the segment spans < 2^24 ns (64*PL*2^24 < 2^32:
-//     no carry chain); wider segments take lane_sums / lane_sums_f64 as fast_body does;
+//     no carry chain); wider segments take lane_sums / lane_sums_f64;
 //   * the squares are packed f32 (v_pk_add / v_pk_fma on sample pairs: d, c < 2^24 convert
 //     exactly, so (float)d - (float)c == (float)(int)(d - c));
 //   * when ranks t0, t1 fall in different buckets b0 < b1, s[t0] = max{d < hi(b0)} and
@@ -527,15 +335,36 @@ struct LeanOut {
     Sd sd;
     double sq;
 };
-
+// LeanOut::sd through a 64-bit register pair (the group epilogues' lane-held results)
+__device__ __forceinline__ uint64_t sd_bits(uint64_t sd) { return sd; }
+__device__ __forceinline__ uint64_t sd_bits(double sd) { return (uint64_t)__double_as_longlong(sd); }
 template <int PL>
-__device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsigned x0,
+__device__ __forceinline__ double sd_value(uint64_t b) {
+    if constexpr (PL <= 16)
+        return (double)b;
+    else
+        return __longlong_as_double((long long)b);
+}
+
+// !FULL: a segment of n < 64 * PL samples starting m0 slots into its first 16-byte vector
+// (finish_loads set every other slot to x0, sample 0, the pivot: neutral for MIN / MAX, d - c
+// = 0 in the squares).  The pad = 64 * PL - n copies of x0 are taken out again where they
+// count: pad * c from the exact sum; -pad as the initial count of the pivot's bin at every
+// histogram level whose window holds it; and from the candidates of the pivot's bucket (a
+// masked compaction, only when the median's bucket is the pivot's).  The wrapped max / min of
+// two buckets need nothing: x0 is a sample, so its copies change neither.
+// KB: level-0 bins kept in registers (PL more VGPRs).
+template <int PL, bool FULL = true, bool KB = (PL <= 16)>
+__device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, int m0, unsigned x0,
                                                  unsigned* hist) {
     using Sd = typename LeanOut<PL>::Sd;
     constexpr int NB = Bins<PL>::NB;
     constexpr int LOGNB = Bins<PL>::LOG;
     constexpr int BPL = Bins<PL>::BPL;
     const int lane = lane_id();
+    const unsigned pad = FULL ? 0u : (unsigned)(64 * PL - n);
+    const int eb = 4 * lane - m0;  // slot of register i: eb + 256 (i >> 2) + (i & 3)
+    const auto real = [&](int i) { return FULL || (unsigned)(eb + 256 * (i >> 2) + (i & 3)) < (unsigned)n; };
 
     unsigned lmn = v[0], lmx = v[0];
 #pragma unroll
@@ -557,7 +386,8 @@ __device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsig
     for (int i = 0; i < PL; ++i) v[i] += off;
 
     // ---- exact sum + squares about the pivot c (lane_sums order: pairs, groups of 16) ----
-    unsigned c = x0 - mn;
+    const unsigned cp = x0 - mn;  // the padding's d
+    unsigned c = cp;
     Sd sd;
     double acc;
     if (range < (1u << 24)) {
@@ -605,19 +435,21 @@ __device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsig
             r += dpp<0x4E>(r);
             r += dpp<0x141>(r);
             r += dpp<0x140>(r);
-            sd = (Sd)(((uint64_t)rl(r, 0) + rl(r, 16)) + ((uint64_t)rl(r, 32) + rl(r, 48)));
+            sd = (Sd)(((uint64_t)rl(r, 0) + rl(r, 16)) + ((uint64_t)rl(r, 32) + rl(r, 48)) -
+                      (uint64_t)pad * cp);
         } else {
-            sd = (Sd)wave_sum_f64_b((double)ls);
+            sd = (Sd)(wave_sum_f64_b((double)ls) - (double)((uint64_t)pad * cp));  // exact
         }
-    } else {  // rare: a ring spanning >= 16.7 ms -- fast_body's sums
+    } else {  // rare: a ring spanning >= 16.7 ms
         uint64_t sdi;
         if (range < 0x80000000u) {
             lane_sums<PL>(v, c, sdi, acc);
         } else {
             c = 0u;
             lane_sums_f64<PL>(v, sdi, acc);
+            if (!FULL) acc -= lane == 0 ? (double)pad * ((double)cp * (double)cp) : 0.0;
         }
-        sd = (Sd)wave_sum_f64_b((double)sdi);
+        sd = (Sd)(wave_sum_f64_b((double)sdi) - (double)((uint64_t)pad * cp));
     }
     const double sq = wave_sum_f64_b(acc);
 
@@ -625,12 +457,27 @@ __device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsig
     // KEEPBIN (short segments, registers to spare): every sample's level-0 bin stays in a
     // register, so the level-0 candidate test is one compare instead of a subtract, a shift
     // and a compare
-    constexpr bool KEEPBIN = PL <= 16;
+    constexpr bool KEEPBIN = KB;
     unsigned hb[KEEPBIN ? PL : 1];
     const int bits = 32 - __clz((int)range);
     int shift = bits > LOGNB ? bits - LOGNB : 0;
+    const unsigned xc = B + cp;  // the padding's value
+    // the padding's bin starts at -pad: at level 0 bin ubfe(x, shift, LOGNB) (the window is
+    // every value; NB << shift may be 2^32), below it [wlo, wlo + NB << shift) if it holds xc
+    const auto clear_bins = [&](unsigned wlo_, int shift_, bool level0) {
+        const unsigned q = xc - wlo_;
+        const unsigned pb = !(!FULL && pad) ? 0xFFFFFFFFu
+                            : level0 ? __builtin_amdgcn_ubfe(xc, (unsigned)shift_, (unsigned)LOGNB)
+                            : q < ((unsigned)NB << shift_) ? q >> shift_ : 0xFFFFFFFFu;
 #pragma unroll
-    for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+        for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = (unsigned)(lane * BPL + j) == pb ? 0u - pad : 0u;
+    };
+    if (FULL) {
+#pragma unroll
+        for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+    } else {
+        clear_bins(B, shift, true);
+    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
@@ -645,8 +492,12 @@ __device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsig
     unsigned wlo = B, below = 0, d0 = 0, d1 = 0;
     for (int level = 0;; ++level) {
         if (level > 0) {
+            if (FULL) {
 #pragma unroll
-            for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+                for (int j = 0; j < BPL; ++j) hist[lane * BPL + j] = 0u;
+            } else {
+                clear_bins(wlo, shift, false);
+            }
             __builtin_amdgcn_wave_barrier();
             const unsigned span = (unsigned)NB << shift;
 #pragma unroll
@@ -689,7 +540,16 @@ __device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, unsig
             unsigned base = 0;
             const unsigned lo0 = wlo + (b0 << shift);
             const unsigned width = 1u << shift;
-            if (KEEPBIN && level == 0) {
+            const bool masked = !FULL && pad && xc - lo0 < width;  // the padding is in bucket b0
+            if (masked) {
+#pragma unroll
+                for (int i = 0; i < PL; ++i) {
+                    const bool in = v[i] - lo0 < width && real(i);
+                    const uint64_t bm = __ballot(in);
+                    if (in) hist[base + mbcnt(bm)] = v[i];
+                    base += (unsigned)__popcll(bm);
+                }
+            } else if (KEEPBIN && level == 0) {
 #pragma unroll
                 for (int i = 0; i < PL; ++i) {
                     const bool in = hb[KEEPBIN ? i : 0] == b0;
@@ -741,14 +601,14 @@ template <int PL>
 __device__ __forceinline__ unsigned lean_body(unsigned (&v)[PL], int n, unsigned x0, int64_t s,
                                           unsigned* hist, const nvrx_stats_soa& out,
                                           const ColRef& cr) {
-    const LeanOut<PL> r = lean_core<PL>(v, n, x0, hist);
+    const LeanOut<PL> r = lean_core<PL>(v, n, 0, x0, hist);
     emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, (double)r.sd, r.sq, r.c, cr);
     return r.mx;
 }
 
 // HBM -> VGPR in two steps, so a caller can issue the next segment's loads before it
 // reduces the current one.  issue_loads: the segment p[0:n) into v (64*PL slots, see
-// fast_body) with 16-byte buffer loads from the 16-B aligned base below p; the descriptor
+// lean_core) with 16-byte buffer loads from the 16-B aligned base below p; the descriptor
 // is built from wave-uniform (readfirstlane'd) inputs so the loads issue back to back (no
 // waterfall); lanes past the segment fall outside the descriptor's range (the hardware
 // returns 0).  finish_loads (after the loads landed): m0 = p's offset in its 16-B vector
@@ -828,8 +688,10 @@ void seg_stats_fast_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     int m0;
     unsigned x0;
     load_segment<PL, FULL>(p, n, v, m0, x0);
-    // returns MAX: keys of >= 3.76 s take the decoded moments (rare, wave-uniform)
-    if (fast_body<PL, FULL>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
+    const LeanOut<PL> r = lean_core<PL, FULL>(v, n, m0, x0, hist);
+    emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, (double)r.sd, r.sq, r.c, cr);
+    // keys of >= 3.76 s take the decoded moments (rare, wave-uniform)
+    if (r.mx >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
 }
 
 // FULL segments only (64*PL samples each, 16-B aligned): lean_body.
@@ -880,7 +742,7 @@ void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, nvrx_stats_
         int m0;
         unsigned x0;
         load_segment<PL, true>(p, n, v, m0, x0);
-        const LeanOut<PL> r = lean_core<PL>(v, n, x0, hist);
+        const LeanOut<PL> r = lean_core<PL>(v, n, 0, x0, hist);
         const uint64_t sqb = (uint64_t)__double_as_longlong(r.sq);
         const bool mine = lane == j;  // one compare, nine selects
         a_mn = mine ? r.mn : a_mn;
@@ -1133,7 +995,7 @@ template <int PL, class Segs>
 static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
                       const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
-    // lean_body: bit-identical to fast_body<PL, true>, 6-9 % faster (tools/mb_c3.hip)
+    // FULL: unmasked lean_core (group epilogue for PL <= 16); otherwise the masked lean_core
     if constexpr (PL <= 16) {
         if (full) {
             const int g = lean_group(nseg);

@@ -11,7 +11,7 @@
 //   n <= 8..128       one LANE per segment: the samples in registers, a sorting
 //                     sorting network, then CuptiProfiler.cpp:53-71 statement by
 //                     statement (sequential f32 sums) -- every field bit-exact
-//   n <= 64*PL        one WAVE per segment (fast_body, segment_kernels.h), PL 4..128
+//   n <= 64*PL        one WAVE per segment (lean_core, segment_kernels.h), PL 4..128
 //   longer / EXACT    one WORKGROUP per segment (exact_body)
 //
 // Classification is three small launches over the segment lengths (count per block,

@@ -202,6 +202,10 @@ struct ListPrefetch {
     static constexpr bool on = PL <= 16;
 };
 template <int PL>
+struct ListKeepBin {  // level-0 bins in registers while they fit beside the prefetch buffer
+    static constexpr bool on = PL <= 8;
+};
+template <int PL>
 struct ListGroup {  // one epilogue per chunk (emit_lane): the short classes, whose chunks are long
     static constexpr bool on = PL <= 8;
 };
@@ -250,8 +254,8 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
         unsigned a_mn = 0, a_mx = 0, a_k0 = 0, a_k1 = 0, a_c = 0, a_sdlo = 0, a_sdhi = 0, a_sqlo = 0,
                  a_sqhi = 0;
         uint32_t wide = 0;
-        const auto keep = [&](int j, const FastOut& r) {
-            const uint64_t sdb = (uint64_t)__double_as_longlong(r.sd);
+        const auto keep = [&](int j, const LeanOut<PL>& r) {
+            const uint64_t sdb = sd_bits(r.sd);
             const uint64_t sqb = (uint64_t)__double_as_longlong(r.sq);
             const bool mine = lane == j;
             a_mn = mine ? r.mn : a_mn;
@@ -280,10 +284,13 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
                 int m0;
                 unsigned x0;
                 finish_loads<PL, false>(p, n, v, m0, x0);
-                if (ListGroup<PL>::on)
-                    keep(j, fast_core<PL, false>(v, n, m0, x0, hist));
-                else if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
-                    wide_moments(p, n, s, out);
+                const LeanOut<PL> r = lean_core<PL, false, ListKeepBin<PL>::on>(v, n, m0, x0, hist);
+                if (ListGroup<PL>::on) {
+                    keep(j, r);
+                } else {
+                    emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, (double)r.sd, r.sq, r.c, cr);
+                    if (r.mx >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
+                }
 #pragma unroll
                 for (int i = 0; i < PL; ++i) v[i] = w[i];
                 s = s2;
@@ -296,15 +303,18 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
                 int m0;
                 unsigned x0;
                 load_segment<PL, false>(p, n, v, m0, x0);
-                if (ListGroup<PL>::on)
-                    keep(j, fast_core<PL, false>(v, n, m0, x0, hist));
-                else if (fast_body<PL, false>(v, n, m0, x0, s, hist, out, cr) >= NVRX_KEY_WIDE)
-                    wide_moments(p, n, s, out);
+                const LeanOut<PL> r = lean_core<PL, false, ListKeepBin<PL>::on>(v, n, m0, x0, hist);
+                if (ListGroup<PL>::on) {
+                    keep(j, r);
+                } else {
+                    emit_stats(out, s, n, r.mn, r.mx, r.d0, r.d1, (double)r.sd, r.sq, r.c, cr);
+                    if (r.mx >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
+                }
             }
         }
         if (ListGroup<PL>::on && lane < m)
             emit_lane(out, (int64_t)sid, nn, a_mn, a_mx, a_k0, a_k1,
-                      __longlong_as_double((long long)(((uint64_t)a_sdhi << 32) | a_sdlo)),
+                      sd_value<PL>(((uint64_t)a_sdhi << 32) | a_sdlo),
                       __longlong_as_double((long long)(((uint64_t)a_sqhi << 32) | a_sqlo)), a_c, cr);
         while (wide) {  // keys of >= 3.76 s: the decoded moments (rare)
             const int j = __builtin_ffs(wide) - 1;
