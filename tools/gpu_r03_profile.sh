@@ -4,7 +4,7 @@
 # Output: gpurun_out/r03_prof/
 set -e
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r03_prof
+OUT=$R/gpurun_out/${PROF_TAG:-r03_prof}
 mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
