@@ -433,8 +433,12 @@ static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* re
     if (fixed + (size_t)RB_WAVES * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)records_bucket_kernel<RB_WAVES, RB_REGS>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
+        const void* k = (const void*)records_bucket_kernel<RB_WAVES, RB_REGS>;
+        hipFuncAttributes fa;
+        hipError_t e = hipFuncGetAttributes(&fa, k);
+        if (e != hipSuccess) return e;
+        if (fa.sharedSizeBytes + RB_LAUNCH_LDS > 160 * 1024) return hipErrorInvalidConfiguration;  // static LDS grew
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
         if (e != hipSuccess) return e;
         attr_set = true;
     }

@@ -2,7 +2,7 @@
 # Masked lean body for ragged / misaligned segments: the full GPU suite, then configs[3] record
 # statistics against tools/ab_pkg, interleaved.  Output: gpurun_out/r03_masked/
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r03_masked
+OUT=$R/gpurun_out/${RUN_TAG:-r03_masked}
 mkdir -p "$OUT"
 cd "$R"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1
