@@ -205,9 +205,14 @@ class MatrixReporter:
         on N GPUs (the partials exchange stays an eager collective)."""
         return ReportGraph(self, ns, s_push)
 
-    def _unpack(self) -> BatchResult:
+    def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False) -> "PipelinedReports":
+        """Reports replayed two deep (1 GPU): report i+1's device work is queued before report
+        i's results are read on the host, each report landing in its own pinned buffer."""
+        return PipelinedReports(self, ns, s_push, timing)
+
+    def _unpack(self, buf: Optional[torch.Tensor] = None) -> BatchResult:
         R = self.R
-        h = self.h_out.numpy()
+        h = (self.h_out if buf is None else buf).numpy()
         gr = h[0:8 * R].view(np.float64).copy() if self.relative else None
         gi = h[8 * R:16 * R].view(np.float64).copy() if self.individual else None
         sr = h[16 * R:17 * R].astype(bool) if self.relative else None
@@ -268,3 +273,73 @@ class ReportGraph:
         self.full.replay()
         _wait(self.rep.device)
         return self.rep._unpack()
+
+
+class PipelinedReports:
+    """Full reports as HIP graphs, two in flight (1 GPU).  Each report -- column-reference init,
+    statistics, scores + straggler masks -- ends with the device-to-host copy of the packed
+    results into one of two pinned buffers, so the host can read report i while report i+1
+    runs: the GPU sees back-to-back reports instead of one report per host round trip.  Report
+    order on the device is the submission order (one stream), so the individual history
+    advances exactly as with report().  timing: the statistics phase is its own graph with
+    timing events recorded around its replay (ROCm's torch refuses events inside a capture);
+    otherwise one graph per report."""
+
+    def __init__(self, rep: MatrixReporter, ns: torch.Tensor, s_push: int, timing: bool = False):
+        if rep.exchange:
+            raise RuntimeError("pipelined reports: 1 GPU (the partials exchange is an eager collective)")
+        self.rep, self.timing = rep, timing
+        d = rep.device
+        side = torch.cuda.Stream(d)
+        side.wait_stream(torch.cuda.current_stream(d))
+        with torch.cuda.stream(side):  # one eager pass: first-launch setup outside the capture
+            rep.compute_stats(ns, s_push)
+            rep.compute_scores()
+        torch.cuda.current_stream(d).wait_stream(side)
+        torch.cuda.synchronize(d)
+        self.bufs = [torch.empty_like(rep.h_out, pin_memory=True) for _ in range(2)]
+        self.stats = None
+        if timing:
+            self.stats = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.stats):
+                rep.compute_stats(ns, s_push)
+            self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(2)]
+        self.graphs = []  # per slot: the rest of the report (timing) or all of it
+        for k in range(2):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                if not timing:
+                    rep.compute_stats(ns, s_push)
+                rep.compute_scores()
+                self.bufs[k].copy_(rep.out, non_blocking=True)
+            self.graphs.append(g)
+        self.done = [torch.cuda.Event() for _ in range(2)]
+        self.pending = []  # slots in flight, oldest first
+        self.n = 0
+
+    def submit(self) -> None:
+        """Queue the next report (at most two in flight: collect() the oldest first)."""
+        if len(self.pending) == 2:
+            raise RuntimeError("two reports in flight: collect() one first")
+        k = self.n & 1
+        if self.timing:
+            self.ev[k][0].record()
+            self.stats.replay()
+            self.ev[k][1].record()
+        self.graphs[k].replay()
+        self.done[k].record()
+        self.pending.append(k)
+        self.n += 1
+
+    def collect(self):
+        """(BatchResult, stats ms or None) of the oldest report in flight, once it landed."""
+        k = self.pending.pop(0)
+        ev = self.done[k]
+        if _SYNC_BLOCK:
+            ev.synchronize()
+        else:
+            while not ev.query():
+                pass
+        ms = self.ev[k][0].elapsed_time(self.ev[k][1]) if self.timing else None
+        return self.rep._unpack(self.bufs[k]), ms
