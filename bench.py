@@ -481,7 +481,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic,
-                         "kernel": "seg_stats_lean_kernel<128>",
+                         "kernel": "seg_stats_lean_group_kernel<128> (4 segments per wave)",
                          "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,

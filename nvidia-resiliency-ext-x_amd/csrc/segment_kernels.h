@@ -723,7 +723,6 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
 template <int PL, class Segs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
 void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, nvrx_stats_soa out, ColRef cr) {
-    static_assert(PL <= 16, "integer sums (LeanOut::Sd) only for PL <= 16");
     constexpr int NB = Bins<PL>::NB;
     __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -750,15 +749,16 @@ void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, nvrx_stats_
         a_k0 = mine ? r.mn + r.d0 : a_k0;
         a_k1 = mine ? r.mn + r.d1 : a_k1;
         a_c = mine ? r.c : a_c;
-        a_sdlo = mine ? (uint32_t)r.sd : a_sdlo;
-        a_sdhi = mine ? (uint32_t)(r.sd >> 32) : a_sdhi;
+        const uint64_t sdb = sd_bits(r.sd);
+        a_sdlo = mine ? (uint32_t)sdb : a_sdlo;
+        a_sdhi = mine ? (uint32_t)(sdb >> 32) : a_sdhi;
         a_sqlo = mine ? (uint32_t)sqb : a_sqlo;
         a_sqhi = mine ? (uint32_t)(sqb >> 32) : a_sqhi;
         if (r.mx >= NVRX_KEY_WIDE) wide |= 1ull << j;
     }
     if (lane < cnt)
         emit_lane(out, s0 + lane, n, a_mn, a_mx, a_k0, a_k1,
-                  (double)(((uint64_t)a_sdhi << 32) | a_sdlo),
+                  sd_value<PL>(((uint64_t)a_sdhi << 32) | a_sdlo),
                   __longlong_as_double((long long)(((uint64_t)a_sqhi << 32) | a_sqlo)), a_c, cr);
     while (wide) {  // keys of >= 3.76 s: the decoded moments (rare)
         const int j = __builtin_ffsll(wide) - 1;
@@ -985,10 +985,21 @@ static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream
     return hipGetLastError();
 }
 
-// segments per wave of the group kernel: up to 64 while the grid keeps >= 32768 waves
+// segments per wave of the group kernel: up to NVRX_LEAN_GROUP_MAX while the grid keeps >= 32768 waves
+// Segments per wave of the group kernel: configs[2] statistics interleaved on one box
+// (tools/build_variant.sh + tools/gpu_r03_variants.sh, profiles/r03/group_size/): 4 / 6 / 8 / 12
+// / 32 / 64 per wave 5.70 / 5.87 / 5.57 / 5.78 / 6.04 / 5.87 ms (round-start library 6.00 ms);
+// a prefetch of the next segment's loads (80 VGPRs, 6 waves / SIMD) 5.90-5.94 at 64.  A build
+// constant, so A/B builds can override it.
+#ifndef NVRX_LEAN_GROUP_MAX
+#define NVRX_LEAN_GROUP_MAX 8
+#endif
+#ifndef NVRX_LEAN_GROUP_PL_MAX  // FULL segments of up to 64 * this many samples take the group kernel
+#define NVRX_LEAN_GROUP_PL_MAX 128
+#endif
 static inline int lean_group(int64_t nseg) {
     const int64_t g = nseg / 32768;
-    return g < 1 ? 1 : g > 64 ? 64 : (int)g;
+    return g < 1 ? 1 : g > NVRX_LEAN_GROUP_MAX ? NVRX_LEAN_GROUP_MAX : (int)g;
 }
 
 template <int PL, class Segs>
@@ -996,7 +1007,7 @@ static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stat
                       const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
     // FULL: unmasked lean_core (group epilogue for PL <= 16); otherwise the masked lean_core
-    if constexpr (PL <= 16) {
+    if constexpr (PL <= NVRX_LEAN_GROUP_PL_MAX) {
         if (full) {
             const int g = lean_group(nseg);
             const int64_t waves = (nseg + g - 1) / g;

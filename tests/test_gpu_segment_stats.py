@@ -351,7 +351,7 @@ def test_grouped_full_segments(n):
     rng = np.random.default_rng(n)
     K = 37
     nseg = K * (3550 if n == 1024 else 3601)
-    group = min(64, max(1, nseg // 32768))
+    group = min(8, max(1, nseg // 32768))  # segment_kernels.h lean_group
     assert group > 1 and nseg % group  # groups of 4 and a partial last group
     host = rng.integers(2000, 2_200_000, size=nseg * n, dtype=np.uint32)
     edges = _edge_segments(n)

@@ -5,7 +5,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "seg_stats_lean_kernel<128, nvrx::StridedSegs"
+KERNEL = "seg_stats_lean_group_kernel<128, nvrx::StridedSegs"
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/round"
 
 
@@ -24,7 +24,7 @@ alg = 4 * 64 * 2048 * 8192 + 24 * 64 * 2048
 hbm = (2 * fetch + write) * 1024
 out = {
     "workload": "c2: 64 ranks x 2048 kernels x 8192 retained samples (S_push 10000)",
-    "kernel": "nvrx::" + KERNEL + ", true>",
+    "kernel": "nvrx::" + KERNEL + ">",
     "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py "
               "--steps 3 --warmup 1); median over dispatches; FETCH_SIZE doubled per "
               "MI355X_MICROARCH.md (gfx950 reports half of wide coalesced streaming reads); KB x 1024",
