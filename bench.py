@@ -114,6 +114,9 @@ def make_shard(R, K_global, s_push, world, rank, dev):
     return ns, kidx
 
 
+TIMED_EVERY = 5  # pipelined reports: one in five times its statistics kernel on an idle device
+
+
 def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True):
     """Full reports on one configuration.  use_graph: every report replays HIP graphs of the
     same kernels (one graph launch instead of one host launch per operation) -- on 1 GPU two
@@ -128,8 +131,9 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
     if use_graph and not rep.exchange:
         # 1 GPU: whole-report graphs two in flight (batch.PipelinedReports) -- report i+1 is
         # queued before report i's results are read on the host; every report lands (D2H +
-        # host unpack) inside the timed region; the stats phase (its own graph) is timed by
-        # events recorded around its replay
+        # host unpack) inside the timed region
+        # every TIMED_EVERY-th report is submitted on an idle device with events around its
+        # statistics graph (PipelinedReports.submit(timed=True))
         pipe = rep.pipelined(ns, s_push, timing=time_kernel)
         for _ in range(max(1, warmup)):
             pipe.submit()
@@ -137,10 +141,10 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         ks = []
         barrier(world)
         t0 = time.perf_counter()
-        pipe.submit()
+        pipe.submit(timed=time_kernel)
         for i in range(steps):
             if i + 1 < steps:
-                pipe.submit()
+                pipe.submit(timed=time_kernel and (i + 1) % TIMED_EVERY == 0)
             res, ms = pipe.collect()
             if ms is not None:
                 ks.append(ms)

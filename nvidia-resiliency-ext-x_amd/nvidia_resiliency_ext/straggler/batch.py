@@ -281,9 +281,11 @@ class PipelinedReports:
     results into one of two pinned buffers, so the host can read report i while report i+1
     runs: the GPU sees back-to-back reports instead of one report per host round trip.  Report
     order on the device is the submission order (one stream), so the individual history
-    advances exactly as with report().  timing: the statistics phase is its own graph with
-    timing events recorded around its replay (ROCm's torch refuses events inside a capture);
-    otherwise one graph per report."""
+    advances exactly as with report().
+    timing: submit(timed=True) first lets the reports in flight finish, then replays the
+    statistics phase as its own graph between two timing events (ROCm's torch refuses events
+    inside a capture) and the rest of the report as another -- a clean measurement of the
+    statistics kernel on an otherwise idle device, for a sample of the reports."""
 
     def __init__(self, rep: MatrixReporter, ns: torch.Tensor, s_push: int, timing: bool = False):
         if rep.exchange:
@@ -298,48 +300,61 @@ class PipelinedReports:
         torch.cuda.current_stream(d).wait_stream(side)
         torch.cuda.synchronize(d)
         self.bufs = [torch.empty_like(rep.h_out, pin_memory=True) for _ in range(2)]
-        self.stats = None
-        if timing:
-            self.stats = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.stats):
-                rep.compute_stats(ns, s_push)
-            self.ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                       for _ in range(2)]
-        self.graphs = []  # per slot: the rest of the report (timing) or all of it
-        for k in range(2):
+
+        def capture(stats: bool, rest: bool, k: int):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                if not timing:
+                if stats:
                     rep.compute_stats(ns, s_push)
-                rep.compute_scores()
-                self.bufs[k].copy_(rep.out, non_blocking=True)
-            self.graphs.append(g)
+                if rest:
+                    rep.compute_scores()
+                    self.bufs[k].copy_(rep.out, non_blocking=True)
+            return g
+
+        self.full = [capture(True, True, k) for k in range(2)]
+        if timing:
+            self.stats = capture(True, False, 0)
+            self.rest = [capture(False, True, k) for k in range(2)]
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.done = [torch.cuda.Event() for _ in range(2)]
-        self.pending = []  # slots in flight, oldest first
+        self.pending = []  # (slot, timed) in flight, oldest first
+        self.ready = []    # results collected early (a timed submit drains), oldest first
         self.n = 0
 
-    def submit(self) -> None:
+    def submit(self, timed: bool = False) -> None:
         """Queue the next report (at most two in flight: collect() the oldest first)."""
         if len(self.pending) == 2:
             raise RuntimeError("two reports in flight: collect() one first")
         k = self.n & 1
-        if self.timing:
-            self.ev[k][0].record()
+        if timed:
+            if not self.timing:
+                raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
+            while self.pending:  # the device idles before the measured statistics phase
+                self.ready.append(self._land())
+            self.ev[0].record()
             self.stats.replay()
-            self.ev[k][1].record()
-        self.graphs[k].replay()
+            self.ev[1].record()
+            self.rest[k].replay()
+        else:
+            self.full[k].replay()
         self.done[k].record()
-        self.pending.append(k)
+        self.pending.append((k, timed))
         self.n += 1
 
-    def collect(self):
-        """(BatchResult, stats ms or None) of the oldest report in flight, once it landed."""
-        k = self.pending.pop(0)
+    def _land(self):
+        k, timed = self.pending.pop(0)
         ev = self.done[k]
         if _SYNC_BLOCK:
             ev.synchronize()
         else:
             while not ev.query():
                 pass
-        ms = self.ev[k][0].elapsed_time(self.ev[k][1]) if self.timing else None
+        ms = self.ev[0].elapsed_time(self.ev[1]) if timed else None
         return self.rep._unpack(self.bufs[k]), ms
+
+    def collect(self):
+        """(BatchResult, statistics ms for a timed report or None) of the oldest report, once it
+        landed."""
+        if self.ready:
+            return self.ready.pop(0)
+        return self._land()

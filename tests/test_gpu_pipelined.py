@@ -25,9 +25,9 @@ def test_pipelined_matches_sequential_reports():
     # b: the same five reports, two in flight; the input changes only between collections
     for i in range(5):
         ns.copy_(seqs[i % 2])
-        pipe.submit()
+        pipe.submit(timed=i % 2 == 0)
         res, ms = pipe.collect()
-        assert ms is not None and ms > 0.0
+        assert (ms is not None and ms > 0.0) if i % 2 == 0 else ms is None
         got.append(res)
     for w, g in zip(want, got):
         np.testing.assert_array_equal(w.gpu_relative, g.gpu_relative)
@@ -46,8 +46,14 @@ def test_pipelined_two_in_flight():
     pipe.submit()
     with pytest.raises(RuntimeError):
         pipe.submit()
-    for _ in range(2):
-        res, ms = pipe.collect()
-        assert ms is None
-        np.testing.assert_array_equal(res.gpu_relative, want.gpu_relative)
+    with pytest.raises(RuntimeError):  # timed reports need timing=True
+        pipe.collect(), pipe.submit(timed=True)
+    pipe2 = rep.pipelined(ns, S, timing=True)
+    pipe2.submit()
+    pipe2.submit()
+    pipe2.collect()
+    pipe2.submit(timed=True)  # drains the one in flight first
+    outs = [pipe2.collect(), pipe2.collect()]
+    assert outs[0][1] is None and outs[1][1] is not None
+    for res, _ in outs + [pipe.collect()]:
         np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
