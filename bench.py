@@ -114,7 +114,7 @@ def make_shard(R, K_global, s_push, world, rank, dev):
     return ns, kidx
 
 
-TIMED_EVERY = 5  # pipelined reports: one in five times its statistics kernel on an idle device
+TIMED_EVERY = 10  # pipelined reports: one in ten times its statistics kernel on an idle device
 
 
 def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True):

@@ -275,6 +275,9 @@ class ReportGraph:
         return self.rep._unpack()
 
 
+TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
+
+
 class PipelinedReports:
     """Full reports as HIP graphs, two in flight (1 GPU).  Each report -- column-reference init,
     statistics, scores + straggler masks -- ends with the device-to-host copy of the packed
@@ -331,6 +334,10 @@ class PipelinedReports:
                 raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
             while self.pending:  # the device idles before the measured statistics phase
                 self.ready.append(self._land())
+            # a short spin keeps the device busy while the host queues the graphs, so the
+            # first event fires right before the statistics phase rather than a graph-launch
+            # latency ahead of it
+            torch.cuda._sleep(TIMED_SPIN_CYCLES)
             self.ev[0].record()
             self.stats.replay()
             self.ev[1].record()
