@@ -1006,20 +1006,20 @@ template <int PL, class Segs>
 static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stats_soa& out,
                       const ColRef& cr, hipStream_t st) {
     const dim3 grid((unsigned)((nseg + 3) / 4)), block(256);
-    // FULL: unmasked lean_core (group epilogue for PL <= 16); otherwise the masked lean_core
-    if constexpr (PL <= NVRX_LEAN_GROUP_PL_MAX) {
-        if (full) {
+    // FULL: unmasked lean_core with the group epilogue (one segment per wave above
+    // NVRX_LEAN_GROUP_PL_MAX, a build-time choice); otherwise the masked lean_core
+    if (full) {
+        if constexpr (PL <= NVRX_LEAN_GROUP_PL_MAX) {
             const int g = lean_group(nseg);
             const int64_t waves = (nseg + g - 1) / g;
             hipLaunchKernelGGL((seg_stats_lean_group_kernel<PL, Segs>), dim3((unsigned)((waves + 3) / 4)),
                                block, 0, st, segs, nseg, g, out, cr);
-            return;
+        } else {
+            hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
         }
-    }
-    if (full)
-        hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
-    else
+    } else {
         hipLaunchKernelGGL((seg_stats_fast_kernel<PL, false, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    }
 }
 
 // need = samples + alignment slack a wave must hold; picks the smallest PL.  `full`
