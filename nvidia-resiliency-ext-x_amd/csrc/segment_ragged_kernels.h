@@ -213,7 +213,10 @@ template <int PL>
 struct ListOcc {  // the prefetch buffer costs PL more VGPRs, the chunk's results nine
     static constexpr int W = PL == 16 ? 6 : PL == 8 ? 7 : OccV<PL, false>::W;
 };
-constexpr int LIST_CHUNK = 16;
+#ifndef NVRX_LIST_CHUNK  // build-time tuning constant (tools/build_variant.sh)
+#define NVRX_LIST_CHUNK 16
+#endif
+constexpr int LIST_CHUNK = NVRX_LIST_CHUNK;
 
 template <int PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ListOcc<PL>::W)))
