@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-end rehearsal: the GPU suite, smoke() and the default bench line, as the driver runs them.
+# Output: gpurun_out/r03_end/
+R=$GRAFT_REPO_ROOT
+OUT=$R/gpurun_out/r03_end
+mkdir -p "$OUT"
+cd "$R"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -20 "$OUT/pytest.log"; exit 1; }
+tail -2 "$OUT/pytest.log"
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
+tail -1 "$OUT/smoke.log"
+timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -20 "$OUT/bench.err"; exit 1; }
+tail -1 "$OUT/bench.json" | cut -c1-300
