@@ -720,14 +720,17 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
 // unit conversions, the f64 quotients and the root, the stores -- runs once per group,
 // lane-parallel with coalesced stores, instead of once per segment on one busy lane (~55 VALU,
 // half of them f64).  Same arithmetic as emit_stats, so the same bits.
+#ifndef NVRX_GROUP_WAVES  // waves per workgroup of the group kernel (build-time tuning constant)
+#define NVRX_GROUP_WAVES 4
+#endif
 template <int PL, class Segs>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
+__global__ __launch_bounds__(64 * NVRX_GROUP_WAVES) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
 void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, nvrx_stats_soa out, ColRef cr) {
     constexpr int NB = Bins<PL>::NB;
-    __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[NVRX_GROUP_WAVES * NB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id();
-    const int64_t s0 = ((int64_t)blockIdx.x * 4 + wave) * group;
+    const int64_t s0 = ((int64_t)blockIdx.x * NVRX_GROUP_WAVES + wave) * group;
     if (s0 >= nseg) return;
     const int cnt = (int)(nseg - s0 < group ? nseg - s0 : group);
     unsigned* hist = lds_hist + wave * NB;
@@ -1012,8 +1015,9 @@ static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stat
         if constexpr (PL <= NVRX_LEAN_GROUP_PL_MAX) {
             const int g = lean_group(nseg);
             const int64_t waves = (nseg + g - 1) / g;
-            hipLaunchKernelGGL((seg_stats_lean_group_kernel<PL, Segs>), dim3((unsigned)((waves + 3) / 4)),
-                               block, 0, st, segs, nseg, g, out, cr);
+            hipLaunchKernelGGL((seg_stats_lean_group_kernel<PL, Segs>),
+                               dim3((unsigned)((waves + NVRX_GROUP_WAVES - 1) / NVRX_GROUP_WAVES)),
+                               dim3(64 * NVRX_GROUP_WAVES), 0, st, segs, nseg, g, out, cr);
         } else {
             hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
         }
