@@ -714,12 +714,12 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
     if (lean_body<PL>(v, n, x0, s, hist, out, cr) >= NVRX_KEY_WIDE) wide_moments(p, n, s, out);
 }
 
-// FULL segments of <= 1024 samples (the configs[2] shape), where the statistics are bound by
-// VALU issue: each wave reduces `group` consecutive segments one after another and keeps what
-// lean_core returns for segment s0 + j in lane j (one compare and nine selects), so the epilogue -- the
-// unit conversions, the f64 quotients and the root, the stores -- runs once per group,
-// lane-parallel with coalesced stores, instead of once per segment on one busy lane (~55 VALU,
-// half of them f64).  Same arithmetic as emit_stats, so the same bits.
+// FULL segments (configs[1] / configs[2]): each wave reduces `group` consecutive segments one
+// after another and keeps what lean_core returns for segment s0 + j in lane j (one compare and
+// nine selects), so the epilogue -- the unit conversions, the f64 quotients and the root, the
+// stores -- runs once per group, lane-parallel with coalesced stores, instead of once per
+// segment on one busy lane (~55 VALU, half of them f64).  Same arithmetic as emit_stats, so the
+// same bits.  Groups of up to 8 (lean_group): the sweep on configs[2] in DESIGN.md section 3.1.
 #ifndef NVRX_GROUP_WAVES  // waves per workgroup of the group kernel (build-time tuning constant)
 #define NVRX_GROUP_WAVES 4
 #endif
