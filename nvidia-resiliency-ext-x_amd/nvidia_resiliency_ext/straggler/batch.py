@@ -337,7 +337,9 @@ class PipelinedReports:
             # a short spin keeps the device busy while the host queues the graphs, so the
             # first event fires right before the statistics phase rather than a graph-launch
             # latency ahead of it
-            torch.cuda._sleep(TIMED_SPIN_CYCLES)
+            spin = getattr(torch.cuda, "_sleep", None)  # torch's spin kernel (private API)
+            if spin is not None:
+                spin(TIMED_SPIN_CYCLES)
             self.ev[0].record()
             self.stats.replay()
             self.ev[1].record()
