@@ -131,17 +131,25 @@ void records_bucket_kernel(
     const int64_t ns_off = pass == 0 ? 0 :
         (int64_t)pass * (((rec_off[gridDim.x] + 3) & ~(int64_t)3) + (int64_t)gridDim.x * stream_slack(RB_PASS_SLOTS));
     const bool pairs = (((uintptr_t)rs) & 15) == 0;
-    // wave w's chunk: [lo, hi), even boundaries
-    const int64_t per = ((n + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
-    const int64_t lo = min(n, per * wave), hi = min(n, lo + per);
+    // The head of the stream -- up to RB_REGS x 64 x RB_WAVES record pairs -- is held in
+    // registers between the passes, the waves sweeping it together (pair (u RB_WAVES + w) 64 +
+    // lane in register u of wave w: 1.36 against 1.45 ms for per-wave chunks in the pass-1
+    // skeleton on configs[3], tools/mb_rb_read.hip); the rest of the stream is split into
+    // per-wave chunks whose heads go to the LDS stash.
+    const int64_t rp = pairs ? min(n >> 1, (int64_t)RB_REGS * 64 * RB_WAVES) : 0;  // register pairs
+    const u32x4* q = (const u32x4*)rs;
+    // wave w's chunk of the rest: [lo, hi), even boundaries
+    const int64_t n_rest = n - 2 * rp;
+    const int64_t per = ((n_rest + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
+    const int64_t lo = 2 * rp + min(n_rest, per * wave), hi = min(n, lo + per);
     const bool wpairs = pairs && ((hi - lo) % 2 == 0);
     // pairs of this wave's chunk held in LDS between the passes (0 when not pair-aligned)
     const int64_t snp = wpairs ? min((hi - lo) >> 1, stash_pairs) : 0;
     u32x4* wstash = stash + wave * stash_pairs;
     const u32x4* wq = (const u32x4*)(rs + lo);
-    // pairs [snp, held) of the chunk are held in registers; records from lo + 2 held re-read
+    // pairs [held, np) of the chunk are read again in pass 2
     const int64_t np = wpairs ? (hi - lo) >> 1 : 0;
-    const int64_t held = wpairs ? min(np, snp + 64 * (int64_t)RB_REGS) : 0;
+    const int64_t held = snp;
     u32x4 reg[RB_REGS > 0 ? RB_REGS : 1];
 
     for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
@@ -157,8 +165,8 @@ void records_bucket_kernel(
     if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
 #pragma unroll
         for (int u = 0; u < RB_REGS; ++u) {
-            const int64_t p = snp + lane + 64 * u;
-            reg[u] = p < held ? __builtin_nontemporal_load(wq + p) : u32x4{~0u, 0u, ~0u, 0u};
+            const int64_t p = ((int64_t)u * RB_WAVES + wave) * 64 + lane;
+            reg[u] = p < rp ? __builtin_nontemporal_load(q + p) : u32x4{~0u, 0u, ~0u, 0u};
         }
     }
     for_pairs(wq, 0, snp, lane, [&](const u32x4& w, int64_t p) {
