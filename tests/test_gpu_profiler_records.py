@@ -454,3 +454,34 @@ def test_records_stats_slot_tables_past_one_pass(nslots, cap):
             assert counts[g] == pushed.size and seg_len[g] == min(pushed.size, cap)
             got = out_ns[seg_off[g]:seg_off[g] + seg_len[g]].view(np.uint32)
             assert np.array_equal(np.sort(got), np.sort(pushed[-cap:]))
+
+
+@pytest.mark.parametrize("cap", [8192, 700])
+def test_records_streams_around_the_register_head(cap):
+    # the bucketing kernel holds the first 16 x 64 x 16 = 16,384 record pairs of a stream in
+    # registers (read by its 16 waves together) and splits the rest into per-wave chunks: streams
+    # of exactly that many records, one more, one fewer, odd lengths, a rest shorter than one
+    # chunk per wave, and unaligned stream starts (after an odd-length stream); rings that
+    # overflow take the ordered walk.  Every field against the oracle.
+    rng = np.random.default_rng(cap + 17)
+    nslots = 97
+    head = 16 * 64 * 16 * 2  # records
+    lens = [head, head + 1, head - 1, head + 2, head + 31, head + 16 * 64 * 2 + 3, 2 * head + 5, 7, 0]
+    recs, off = [], [0]
+    for n in lens:
+        slot = (rng.zipf(1.3, n) - 1) % nslots
+        ns = rng.integers(1000, 3_000_000, n)
+        recs.append(np.stack([slot, ns], 1).astype(np.uint32))
+        off.append(off[-1] + n)
+    recs = np.concatenate(recs)
+    off = np.array(off, np.int64)
+    d_recs = torch.from_numpy(np.ascontiguousarray(recs).view(np.int32)).cuda()
+    d_off = torch.from_numpy(off).cuda()
+    max_len = int(np.diff(off).max())
+    st = ops.records_stats(d_recs, d_off, nslots, cap, max(1, min(max_len, cap) if cap else max_len),
+                           mode=ops.STATS_FAST).cpu()
+    ref = O.records_stats(recs, off, nslots, cap=cap, nthreads=4)
+    for f in ("num", "min", "max", "med"):
+        assert np.array_equal(getattr(st, f).numpy().view(np.int32), ref[f].view(np.int32)), f
+    xm, xs = O.records_moments(recs, off, nslots, cap=cap, nthreads=4)
+    check_avg_std(st.avg.numpy(), st.std.numpy(), ref, xm, xs, f"register head cap={cap}")
