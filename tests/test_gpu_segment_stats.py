@@ -342,17 +342,17 @@ def test_ragged_class_boundaries(mode, aligned16):
             assert abs(got[4] - v.std() / 1000) <= 1e-6 * v.std() / 1000 + 1e-6 or got[4] == want[4], (s, L)
 
 
-@pytest.mark.parametrize("n", [256, 512, 1024])
-def test_grouped_full_segments(n):
+@pytest.mark.parametrize("n,mult", [(256, 3601), (512, 3601), (1024, 3550), (256, 7087)])
+def test_grouped_full_segments(n, mult):
     """Full segments of <= 1024 samples run the group kernel (several segments per wave, the
     epilogue once per group, lane-parallel): enough segments for groups of > 1 (nseg / 32768),
     a partial last group, the edge distributions (full 32-bit range = wide keys, clusters,
     zeros) at the first, last and middle positions of groups, and the fused column reference."""
     rng = np.random.default_rng(n)
     K = 37
-    nseg = K * (3550 if n == 1024 else 3601)
+    nseg = K * mult
     group = min(8, max(1, nseg // 32768))  # segment_kernels.h lean_group
-    assert group > 1 and nseg % group  # groups of 4 and a partial last group
+    assert group > 1 and nseg % group  # groups of 4 or 8 and a partial last group
     host = rng.integers(2000, 2_200_000, size=nseg * n, dtype=np.uint32)
     edges = _edge_segments(n)
     where = [0, group - 1, group, 5 * group + group // 2, nseg - 1, nseg - group, 3 * group - 1,
