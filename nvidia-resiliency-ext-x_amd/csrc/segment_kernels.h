@@ -643,7 +643,9 @@ __device__ __forceinline__ void finish_loads(const uint32_t* p, int n, unsigned 
     m0 = FULL ? 0 : (int)(((uintptr_t)p & 15) >> 2);
     const unsigned e0 = m0 == 0 ? v[0] : m0 == 1 ? v[1] : m0 == 2 ? v[2] : v[3];
     x0 = __builtin_amdgcn_readlane(e0, 0);
-    if (!FULL) {
+    // a masked-class segment that happens to fill the wave exactly (configs[3]: every ring at
+    // cap = 8192) needs no masking (wave-uniform test)
+    if (!FULL && (n != 64 * PL || m0 != 0)) {
 #pragma unroll
         for (int i = 0; i < PL; ++i) {
             const unsigned e = (unsigned)(((i >> 2) * 64 + lane) * 4 + (i & 3) - m0);
