@@ -114,7 +114,7 @@ def make_shard(R, K_global, s_push, world, rank, dev):
     return ns, kidx
 
 
-TIMED_EVERY = 10  # pipelined reports: one in ten times its statistics kernel on an idle device
+TIMED_REPORTS = 10  # statistics-kernel timing phase after the throughput loop
 
 
 def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True):
@@ -130,26 +130,31 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         res = rep.report(ns, s_push)
     if use_graph and not rep.exchange:
         # 1 GPU: whole-report graphs two in flight (batch.PipelinedReports) -- report i+1 is
-        # queued before report i's results are read on the host; every report lands (D2H +
-        # host unpack) inside the timed region
-        # every TIMED_EVERY-th report is submitted on an idle device with events around its
-        # statistics graph (PipelinedReports.submit(timed=True))
+        # queued before report i's results are read on the host; every report lands (host
+        # unpack of the results the scores kernel wrote to pinned memory) inside the timed
+        # region, which holds nothing but back-to-back reports
         pipe = rep.pipelined(ns, s_push, timing=time_kernel)
         for _ in range(max(1, warmup)):
             pipe.submit()
             res, _ = pipe.collect()
-        ks = []
         barrier(world)
         t0 = time.perf_counter()
-        pipe.submit(timed=time_kernel)
+        pipe.submit()
         for i in range(steps):
             if i + 1 < steps:
-                pipe.submit(timed=time_kernel and (i + 1) % TIMED_EVERY == 0)
-            res, ms = pipe.collect()
-            if ms is not None:
-                ks.append(ms)
+                pipe.submit()
+            res, _ = pipe.collect()
         barrier(world)
         elapsed = time.perf_counter() - t0
+        # the roofline's kernel time: after the throughput loop, same process and buffers,
+        # reports submitted on an idle device with HIP events around the statistics phase
+        ks = []
+        if time_kernel:
+            for _ in range(TIMED_REPORTS):
+                pipe.submit(timed=True)
+                res_t, ms = pipe.collect()
+                ks.append(ms)
+            barrier(world)
         keep = min(s_push, cap)
         return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed,
                     kern_ms=float(np.mean(ks)) if ks else None,

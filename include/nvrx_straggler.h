@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NVRX_ABI_VERSION 3
+#define NVRX_ABI_VERSION 4
 
 #define NVRX_OK 0
 #define NVRX_ERR_INVALID -1   /* bad argument / shape */
@@ -51,9 +51,15 @@ extern "C" {
 /* statistics modes */
 #define NVRX_STATS_FAST 0  /* NUM/MIN/MAX/MED bit-exact; AVG/STD exact mean/std rounded once to f32 */
 #define NVRX_STATS_EXACT 1 /* every field bit-exact with computeStats (sequential f32 over sorted) */
+/* flag OR-ed into the mode of nvrx_segment_stats_strided: col_ref already holds the initial
+ * column reference (+inf bits | 0), e.g. re-initialised by the previous report's nvrx_scores
+ * (nvrx_score_args.reset_col_ref), so the initialising launch is skipped */
+#define NVRX_STATS_COLREF_READY 0x10
 
-/* largest retained segment (statsMaxLenPerKernel) the kernels accept */
-#define NVRX_MAX_SEGMENT 32768
+/* largest retained segment (statsMaxLenPerKernel) the kernels accept.  The reference's ring takes
+ * any capacity (CuptiProfiler.h:49-51); rings of up to 32,768 samples are sorted on chip, longer
+ * ones in device scratch (slower, same bits). */
+#define NVRX_MAX_SEGMENT (1 << 30)
 
 /* SoA output of the statistics kernels: one entry per segment (device pointers).
  * Units are microseconds as float32, like KernelStats (CuptiProfiler.h:39-45). */
@@ -98,6 +104,14 @@ typedef struct nvrx_score_args {
     double* gpu_ind;
     uint8_t* strag_rel;
     uint8_t* strag_ind;
+    /* optional self-resetting epilogue, for reports replayed back to back (HIP graphs): with
+     * `done` (2 u32 of device memory, zero before the first call) the error bits collect in
+     * done[1] and the LAST workgroup to finish stores them to *err (no zeroing of *err needed
+     * before the call), re-initialises reset_col_ref[0 : 2*reset_ncols] to the initial column
+     * reference for the next report's statistics (NVRX_STATS_COLREF_READY) and zeroes done. */
+    uint32_t* done;
+    uint32_t* reset_col_ref;
+    int64_t reset_ncols;
 } nvrx_score_args;
 
 /* ---------------------------------------------------------------- library */
@@ -113,10 +127,16 @@ int nvrx_sync(void* stream);                   /* synchronous: waits for `stream
  * above it (0xE0000000 + bits(f32(ns)) - bits(f32(0xE0000000)), at most 0xF0200000), so it
  * keeps exactly what the reference keeps for any u64 duration, and keys order like the
  * durations.  nvrx_duration_key encodes one (host); a tracer feeding nvrx_profiler_ingest or a
- * matrix of durations of 3.76 s and more must encode them.  Below 3.76 s keys are plain ns. */
+ * matrix of durations of 3.76 s and more must encode them.  Below 3.76 s keys are plain ns.
+ * Every u32 is read as a key: a RAW u32 ns of 3.76 s or more (never encoded) would be read as
+ * the f32 bits of a far larger duration, so nvrx_encode_ns_u32 turns a device array of raw u32
+ * ns into keys in place first.  u32 values above NVRX_KEY_MAX come from no u64 duration (they
+ * decode beyond 2^64 ns, keeping the order). */
 #define NVRX_KEY_WIDE 0xE0000000u
 #define NVRX_KEY_WIDE_F32BITS 0x4F600000u /* bits of f32(0xE0000000) */
+#define NVRX_KEY_MAX 0xF0200000u          /* key of f32(2^64 - 1) */
 uint32_t nvrx_duration_key(uint64_t ns);
+int nvrx_encode_ns_u32(uint32_t* ns, int64_t n, void* stream);
 
 /* ---------------------------------------------------------------- statistics */
 /* Segment s = ns[s*seg_stride + seg_begin : + seg_len] (uint32 duration keys); the
@@ -256,8 +276,8 @@ int nvrx_profiler_generation(nvrx_profiler* p, uint64_t* generation);
  * it; later profiler calls order themselves after it.  Ignored while stopped.  `generation`
  * must be the current nvrx_profiler_generation (NVRX_ERR_STATE otherwise: the slots were
  * numbered before a reset).  Records whose slot is not registered at this call are dropped
- * (never counted, even if that slot number is handed out later).  (While a live capture is
- * started, the copy is itself a kernel dispatch and is recorded like any other.)  No
+ * (never counted, even if that slot number is handed out later).  The copy is the library's
+ * own kernel: a live capture leaves it out.  No
  * reference counterpart: the device-side entry of an external tracer (SURVEY 8(b)
  * nvrx_ingest_records). */
 int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n,
@@ -285,8 +305,11 @@ int nvrx_profiler_get_records(nvrx_profiler* p, int64_t cap_out, int64_t* count,
  * before the process's first HIP call (NVRX_ERR_STATE otherwise).  Once the runtime has
  * initialised, nvrx_profiler_capture_available() returns 1 and every kernel that completes
  * while a profiler handle is started is pushed into it under the reference's composite key
- * "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled name, block dims, grid dims in blocks) with its
- * integer-ns duration; nvrx_profiler_stop / _get_stats flush the capture buffer first. */
+ * "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled name, block dims, grid dims in blocks, a partial
+ * last block counted) with its integer-ns duration; nvrx_profiler_stop / _get_stats flush the
+ * capture buffer first.  As CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL does (CuptiProfiler.cpp:118,
+ * 179), copies and fills are not kernels: the ROCm runtime's blit kernels ("__amd_rocclr_*",
+ * which carry out hipMemcpy* / hipMemset*) are left out unless NVRX_CAPTURE_RUNTIME_KERNELS=1. */
 int nvrx_capture_configure(void);
 int nvrx_profiler_capture_available(void);
 /* Deliver the dispatch records completed so far to the started / stopped profiler
@@ -296,9 +319,14 @@ int nvrx_capture_flush(void);
  * callbacks delivered by rocprofiler-sdk, record headers in them, dispatch records handed to a
  * profiler, wall time spent inside this library's buffer callback, and the number and wall time
  * of rocprofiler_flush_buffer calls (report-time flushes).  No reference counterpart (CUPTI's
- * cost is not exposed either); tools/capture_cost.py reads it.  All zero without capture. */
+ * cost is not exposed either); tools/capture_cost.cpp reads it.  runtime_kernels counts the runtime
+ * blit dispatches left out (above), own_kernels the library's own report kernels left out: while
+ * get_stats / get_records / reset / ingest run, the dispatches of the calling thread are marked
+ * (a rocprofiler-sdk external correlation id) and not captured, while other threads' kernels
+ * still are, as CUPTI keeps its activity enabled through getStats.  All zero without capture. */
 typedef struct nvrx_capture_counters {
-    int64_t callbacks, headers, dispatches, callback_ns, flushes, flush_ns;
+    int64_t callbacks, headers, dispatches, callback_ns, flushes, flush_ns, runtime_kernels,
+        own_kernels;
 } nvrx_capture_counters;
 int nvrx_capture_stats(nvrx_capture_counters* out);
 

@@ -58,6 +58,11 @@ uint32_t nvrx_duration_key(uint64_t ns) {
 }
 int nvrx_abi_version(void) { return NVRX_ABI_VERSION; }
 
+int nvrx_encode_ns_u32(uint32_t* ns, int64_t n, void* stream) {
+    NVRX_CHECK_ARG(n >= 0 && (n == 0 || ns), "nvrx_encode_ns_u32: bad args");
+    return hip_status(nvrx::encode_ns_u32(ns, n, S(stream)), "nvrx_encode_ns_u32");
+}
+
 int nvrx_device_count(int* count) {
     NVRX_CHECK_ARG(count, "nvrx_device_count: null count");
     int c = 0;
@@ -79,13 +84,14 @@ int nvrx_segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_str
     NVRX_CHECK_ARG(nseg >= 0 && seg_len >= 0 && seg_begin >= 0 && seg_stride >= 0,
                    "nvrx_segment_stats_strided: negative size");
     NVRX_CHECK_ARG(nseg == 0 || seg_len == 0 || ns, "nvrx_segment_stats_strided: null ns");
-    NVRX_CHECK_ARG(mode == NVRX_STATS_FAST || mode == NVRX_STATS_EXACT,
+    NVRX_CHECK_ARG((mode & ~NVRX_STATS_COLREF_READY) == NVRX_STATS_FAST ||
+                       (mode & ~NVRX_STATS_COLREF_READY) == NVRX_STATS_EXACT,
                    "nvrx_segment_stats_strided: unknown mode");
     NVRX_CHECK_ARG(nseg <= 1 || seg_stride >= seg_begin + seg_len,
                    "nvrx_segment_stats_strided: segments overlap (stride < begin + len)");
     const int64_t keep = (cap > 0 && seg_len > cap) ? cap : seg_len;
     NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT,
-                   "nvrx_segment_stats_strided: retained segment longer than NVRX_MAX_SEGMENT");
+                   "nvrx_segment_stats_strided: retained segment longer than NVRX_MAX_SEGMENT (2^30)");
     NVRX_CHECK_ARG(nseg < (int64_t)1 << 33, "nvrx_segment_stats_strided: too many segments");
     NVRX_CHECK_ARG(!col_ref || (ncols > 0 && nseg % ncols == 0),
                    "nvrx_segment_stats_strided: col_ref needs ncols > 0 dividing nseg");
@@ -106,7 +112,7 @@ int nvrx_segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, const 
                    "nvrx_segment_stats_ragged: unknown mode");
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
     NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT,
-                   "nvrx_segment_stats_ragged: retained segment longer than NVRX_MAX_SEGMENT");
+                   "nvrx_segment_stats_ragged: retained segment longer than NVRX_MAX_SEGMENT (2^30)");
     NVRX_CHECK_ARG(nseg < (int64_t)1 << 31, "nvrx_segment_stats_ragged: too many segments");
     NVRX_CHECK_ARG(!col_ref || (ncols > 0 && nseg % ncols == 0),
                    "nvrx_segment_stats_ragged: col_ref needs ncols > 0 dividing nseg");
@@ -146,6 +152,8 @@ int nvrx_scores(const nvrx_score_args* a, void* stream) {
     NVRX_CHECK_ARG(!a->hist_index || a->hist_stride > 0,
                    "nvrx_scores: hist_index requires hist_stride");
     NVRX_CHECK_ARG(a->value_f64 == 0 || a->value_f64 == 1, "nvrx_scores: bad value_f64");
+    NVRX_CHECK_ARG(a->reset_ncols >= 0 && (a->reset_ncols == 0 || (a->reset_col_ref && a->done)),
+                   "nvrx_scores: reset_col_ref needs done and reset_ncols >= 0");
     return hip_status(nvrx::scores(*a, S(stream)), "nvrx_scores");
 }
 
@@ -207,7 +215,7 @@ int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t 
     NVRX_CHECK_ARG(nstreams * nslots < (int64_t)1 << 31, "nvrx_records_stats: too many segments");
     NVRX_CHECK_ARG(((uintptr_t)out_ns & 15) == 0, "nvrx_records_stats: out_ns not 16-byte aligned");
     const int64_t keep = (cap > 0 && max_len > cap) ? cap : max_len;
-    NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT, "nvrx_records_stats: retained run longer than NVRX_MAX_SEGMENT");
+    NVRX_CHECK_ARG(keep <= NVRX_MAX_SEGMENT, "nvrx_records_stats: retained run longer than NVRX_MAX_SEGMENT (2^30)");
     return hip_status(nvrx::records_stats(recs, rec_off, nstreams, nslots, cap, mode, max_len,
                                           seg_off, seg_len, out_ns, counts, *out, col_ref, S(stream)),
                       "nvrx_records_stats");
@@ -235,6 +243,7 @@ int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t
 struct nvrx_profiler {
     nvrx_profiler_config cfg{};
     std::mutex mu;
+    std::mutex ctx_mu;  // start / stop against a report's capture pause (CaptureSelf fallback)
     bool initialized = false;
     bool started = false;
     // kernels seen since the last reset (the keys of CuptiProfiler's _kernelDurations map,
@@ -441,25 +450,40 @@ int flush_locked(nvrx_profiler* p) {
     return NVRX_OK;
 }
 
-// While the live capture is started, a report pauses it: the dispatch context is stopped
-// (~10 us) before the flush and the device work and started again after, so the report's own
-// kernels (bucketing, statistics, copies) are not captured as dispatches of the profiled job --
-// the reference's getStats runs on the host and adds nothing.  It does not make the flush
-// cheaper: rocprofiler_flush_buffer takes ~3.5-5 ms whenever records are pending, started or
-// stopped, and ~30 us when none are (tools/capture_cost.cpp, profiles/r03/capture_cost.json).
-struct CapturePause {
+// The report's own kernels (bucketing, statistics, copies) must not be captured as dispatches
+// of the profiled job -- the reference's getStats runs on the host and adds nothing.  They are
+// marked by thread (capture_self_begin: rocprofiler-sdk's external correlation id of every
+// dispatch this thread makes until the guard ends), so kernels that OTHER threads launch during
+// the report are still captured, as CUPTI keeps its activity enabled through getStats.  If the
+// marking is unavailable, the dispatch context is paused instead (kernels other threads launch
+// meanwhile are then lost); start / stop wait for a pause to end (ctx_mu), and the capture is
+// restarted only if the profiler is still started.  Neither makes the flush cheaper
+// (rocprofiler_flush_buffer).
+struct CaptureSelf {
     nvrx_profiler* p;
-    bool paused = false;
-    explicit CapturePause(nvrx_profiler* q) : p(q) {
+    bool marked = false, paused = false;
+    std::unique_lock<std::mutex> ctx;
+    explicit CaptureSelf(nvrx_profiler* q) : p(q) {
+        if (!nvrx::capture_ready()) return;
+        marked = nvrx::capture_self_begin();
+        if (marked) return;
+        ctx = std::unique_lock<std::mutex>(p->ctx_mu);
         bool started;
         {
             std::lock_guard<std::mutex> lk(p->mu);
             started = p->started;
         }
-        if (started && nvrx::capture_ready()) paused = nvrx::capture_stop(p) == 0;
+        if (started) paused = nvrx::capture_stop(p) == 0;
     }
-    ~CapturePause() {
-        if (paused) (void)nvrx::capture_start(p);
+    ~CaptureSelf() {
+        if (marked) nvrx::capture_self_end();
+        if (!paused) return;
+        bool started;
+        {
+            std::lock_guard<std::mutex> lk(p->mu);
+            started = p->started;
+        }
+        if (started) (void)nvrx::capture_start(p);
     }
 };
 
@@ -511,7 +535,7 @@ int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
     NVRX_CHECK_ARG(cfg && out, "nvrx_profiler_create: null argument");
     NVRX_CHECK_ARG(cfg->stats_max_len_per_kernel > 0 &&
                        cfg->stats_max_len_per_kernel <= NVRX_MAX_SEGMENT,
-                   "nvrx_profiler_create: statsMaxLenPerKernel must be in [1, NVRX_MAX_SEGMENT]");
+                   "nvrx_profiler_create: statsMaxLenPerKernel must be in [1, 2^30]");
     NVRX_CHECK_ARG(cfg->mode == NVRX_STATS_FAST || cfg->mode == NVRX_STATS_EXACT,
                    "nvrx_profiler_create: unknown mode");
     std::lock_guard<std::mutex> lk(g_instance_mu);
@@ -580,6 +604,7 @@ int nvrx_profiler_shutdown(nvrx_profiler* p) {
 
 int nvrx_profiler_start(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_start: null handle");
+    std::lock_guard<std::mutex> ctx(p->ctx_mu);  // not inside a report's pause
     {
         std::lock_guard<std::mutex> lk(p->mu);
         if (p->started) std::fprintf(stderr, "CuptiProfiler::startProfiling subsequent call.\n");
@@ -593,6 +618,7 @@ int nvrx_profiler_start(nvrx_profiler* p) {
 
 int nvrx_profiler_stop(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_stop: null handle");
+    std::lock_guard<std::mutex> ctx(p->ctx_mu);  // not inside a report's pause
     const int rc = nvrx::capture_stop(p);
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->started) std::fprintf(stderr, "CuptiProfiler::stopProfiling called while not profiling.\n");
@@ -606,7 +632,7 @@ int nvrx_profiler_stop(nvrx_profiler* p) {
 
 int nvrx_profiler_reset(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_reset: null handle");
-    CapturePause pause(p);
+    CaptureSelf self(p);
     (void)nvrx::capture_flush();  // CuptiProfiler.cpp:149: flush, then clear (outside the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);
@@ -660,6 +686,7 @@ int nvrx_profiler_push(nvrx_profiler* p, const nvrx_record* recs, int64_t n) {
 int nvrx_profiler_ingest(nvrx_profiler* p, const nvrx_record* dev_recs, int64_t n,
                          uint64_t generation, void* stream) {
     NVRX_CHECK_ARG(p && n >= 0 && (n == 0 || dev_recs), "nvrx_profiler_ingest: bad arguments");
+    CaptureSelf self(p);  // the ingest copy is the library's own kernel, not the job's
     std::lock_guard<std::mutex> lk(p->mu);
     if (generation != p->generation)
         return fail(NVRX_ERR_STATE, "nvrx_profiler_ingest: slots of another generation (a reset "
@@ -691,7 +718,7 @@ int nvrx_profiler_saturated(nvrx_profiler* p, int64_t* count) {
 int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, uint32_t* slots,
                             int32_t* num, float* mn, float* mx, float* med, float* avg, float* sd) {
     NVRX_CHECK_ARG(p && count && cap_out >= 0, "nvrx_profiler_get_stats: bad arguments");
-    CapturePause pause(p);  // the report's own kernels are not captured
+    CaptureSelf self(p);  // the report's own kernels are not captured
     (void)nvrx::capture_flush();  // CuptiProfiler.cpp:138 cuptiActivityFlushAll (before the lock)
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);
@@ -761,7 +788,7 @@ int nvrx_profiler_get_records(nvrx_profiler* p, int64_t cap_out, int64_t* count,
                               nvrx_record* out) {
     NVRX_CHECK_ARG(p && count && cap_out >= 0 && (cap_out == 0 || out),
                    "nvrx_profiler_get_records: bad arguments");
-    CapturePause pause(p);
+    CaptureSelf self(p);
     (void)nvrx::capture_flush();
     std::lock_guard<std::mutex> lk(p->mu);
     DeviceGuard g(p->cfg.device);

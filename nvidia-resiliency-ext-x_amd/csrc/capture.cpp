@@ -16,6 +16,7 @@
 // rocprofiler-sdk tools configure when the ROCm runtime initialises: nvrx_capture_configure
 // must run before the process's first HIP call (the Python side does it at
 // KernelProfiler(capture=True) construction and reports whether it took effect).
+#include <rocprofiler-sdk/external_correlation.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
@@ -48,6 +49,13 @@ struct Capture {
     // cost accounting (nvrx_capture_stats): callbacks, headers, dispatch records handed to the
     // profiler, time inside our callback, flushes and time inside rocprofiler_flush_buffer
     std::atomic<uint64_t> n_cb{0}, n_rec{0}, n_pushed{0}, cb_ns{0}, n_flush{0}, flush_ns{0};
+    std::atomic<uint64_t> n_runtime{0};  // runtime copy / fill dispatches left out (below)
+    bool keep_runtime = false;           // NVRX_CAPTURE_RUNTIME_KERNELS=1 keeps them
+    // the library's own report kernels (get_stats / get_records / reset / ingest) are marked
+    // through an external correlation id set for the reporting thread only and left out
+    std::atomic<uint64_t> n_own{0};
+    std::atomic<uint64_t> self_tid{0};  // rocprofiler thread id of the report in progress (0: none)
+    bool self_marking = false;          // the external correlation id request service is on
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -68,6 +76,44 @@ void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_us
     if (n.size() > 3 && n.compare(n.size() - 3, 3, ".kd") == 0) n.resize(n.size() - 3);
     std::lock_guard<std::mutex> lk(cap().mu);
     cap().names[d->kernel_id] = std::move(n);
+}
+
+// The reference's getStats runs on the host and adds no activity of its own; this library's
+// report runs HIP kernels.  They are told apart from the job's by thread: while a report is in
+// progress on thread T, rocprofiler-sdk's request for the external correlation id of a kernel
+// dispatch made on T gets SELF_MARK, and the buffer callback drops those records.  Kernels other
+// threads launch meanwhile keep being captured, as CUPTI keeps its activity enabled through
+// getStats (a pause of the whole dispatch context would lose them).
+constexpr uint64_t SELF_MARK = 0x4E56525853454C46ull;  // "NVRXSELF"
+
+int external_corr_request(rocprofiler_thread_id_t tid, rocprofiler_context_id_t,
+                          rocprofiler_external_correlation_id_request_kind_t, rocprofiler_tracing_operation_t,
+                          uint64_t, rocprofiler_user_data_t* value, void*) {
+    const uint64_t self = cap().self_tid.load(std::memory_order_acquire);
+    if (self != 0 && tid == self) {
+        value->value = SELF_MARK;
+        return 0;
+    }
+    return 1;  // no value of ours: the thread's pushed default (none)
+}
+
+// The reference enables only CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL (CuptiProfiler.cpp:118) and
+// keeps only those records (:179): memcpy and memset are other activity kinds and never reach the
+// kernel summaries.  On ROCm, hipMemcpy*/hipMemset* (and torch's same-device copy_, which takes
+// hipMemcpyAsync) are carried out by the runtime's own blit kernels, which rocprofiler-sdk reports
+// as KERNEL_DISPATCH records like any other; their symbols carry the "__amd_rocclr_" prefix.
+bool runtime_blit_name(const std::string& n) { return n.compare(0, 13, "__amd_rocclr_") == 0; }
+
+// is kernel_id one of those blits?  The name is registered at code-object load, before any
+// dispatch of it; each delivery thread caches the answer so the lock is taken once per kernel.
+bool runtime_blit(uint64_t kernel_id) {
+    thread_local std::unordered_map<uint64_t, bool> known;
+    auto it = known.find(kernel_id);
+    if (it != known.end()) return it->second;
+    std::lock_guard<std::mutex> lk(cap().mu);
+    auto nt = cap().names.find(kernel_id);
+    if (nt == cap().names.end()) return false;  // not registered (yet): keep, do not cache
+    return known[kernel_id] = runtime_blit_name(nt->second);
 }
 
 // CuptiProfiler.cpp:182-185: "%s_blk_%d_%d_%d_grid_%d_%d_%d" (only for a key the profiler
@@ -97,6 +143,7 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
     if (p) {
         thread_local std::vector<nvrx::DispatchRec> batch;
         batch.clear();
+        uint64_t runtime = 0, own = 0;
         for (size_t i = 0; i < num_headers; ++i) {
             const rocprofiler_record_header_t* h = headers[i];
             if (h->category != ROCPROFILER_BUFFER_CATEGORY_TRACING ||
@@ -104,17 +151,32 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
                 continue;
             auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
             const rocprofiler_kernel_dispatch_info_t& di = r->dispatch_info;
-            // block dims = workgroup size; grid_size is in work-items, CUPTI's grid in blocks
+            if (r->correlation_id.external.value == SELF_MARK) {  // a report kernel of ours
+                ++own;
+                continue;
+            }
+            if (!c.keep_runtime && runtime_blit(di.kernel_id)) {
+                ++runtime;
+                continue;
+            }
+            // block dims = workgroup size; grid_size is in work-items, CUPTI's gridX..Z count
+            // blocks, including a partial last block (a module / ext launch whose global size is
+            // not a multiple of the workgroup): ceil
             const uint32_t bx = di.workgroup_size.x, by = di.workgroup_size.y, bz = di.workgroup_size.z;
+            auto blocks = [](uint32_t g, uint32_t b) -> uint32_t {
+                return b ? (uint32_t)(((uint64_t)g + b - 1) / b) : 0;
+            };
             nvrx::DispatchRec d;
-            d.key = {di.kernel_id, bx, by, bz, bx ? di.grid_size.x / bx : 0,
-                     by ? di.grid_size.y / by : 0, bz ? di.grid_size.z / bz : 0};
+            d.key = {di.kernel_id, bx, by, bz, blocks(di.grid_size.x, bx), blocks(di.grid_size.y, by),
+                     blocks(di.grid_size.z, bz)};
             d.ns = r->end_timestamp > r->start_timestamp ? r->end_timestamp - r->start_timestamp : 0;
             batch.push_back(d);
         }
         c.n_cb.fetch_add(1);
         c.n_rec.fetch_add(num_headers);
         c.n_pushed.fetch_add(batch.size());
+        c.n_runtime.fetch_add(runtime);
+        c.n_own.fetch_add(own);
         if (!batch.empty()) nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
     }
     c.cb_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -131,6 +193,13 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
                                                        nullptr) != ROCPROFILER_STATUS_SUCCESS)
         return -1;
     if (rocprofiler_create_context(&c.disp_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+    if (const char* k = std::getenv("NVRX_CAPTURE_RUNTIME_KERNELS")) c.keep_runtime = std::atoi(k) != 0;
+    {
+        const rocprofiler_external_correlation_id_request_kind_t kinds[] = {
+            ROCPROFILER_EXTERNAL_CORRELATION_REQUEST_KERNEL_DISPATCH};
+        c.self_marking = rocprofiler_configure_external_correlation_id_request_service(
+                             c.disp_ctx, kinds, 1, external_corr_request, nullptr) == ROCPROFILER_STATUS_SUCCESS;
+    }
     size_t watermark = 1u << 20;  // ~ the Detector's CUPTI bufferSize (1 MB, cupti.py:25)
     // NVRX_CAPTURE_WATERMARK overrides it, not below 64 KiB: with watermarks of a few KB
     // rocprofiler-sdk (ROCm 7.2) was measured to lose dispatch records (tools/diag_capture.py)
@@ -202,6 +271,17 @@ int capture_flush() {
     return ok ? 0 : -1;
 }
 
+bool capture_self_begin() {
+    Capture& c = cap();
+    if (!c.ready || !c.self_marking) return false;
+    rocprofiler_thread_id_t tid = 0;
+    if (rocprofiler_get_thread_id(&tid) != ROCPROFILER_STATUS_SUCCESS || tid == 0) return false;
+    c.self_tid.store(tid, std::memory_order_release);
+    return true;
+}
+
+void capture_self_end() { cap().self_tid.store(0, std::memory_order_release); }
+
 void capture_detach(nvrx_profiler* p) {
     Capture& c = cap();
     if (c.target.load() != p) return;
@@ -244,6 +324,8 @@ int nvrx_capture_stats(nvrx_capture_counters* out) {
     out->callback_ns = (int64_t)c.cb_ns.load();
     out->flushes = (int64_t)c.n_flush.load();
     out->flush_ns = (int64_t)c.flush_ns.load();
+    out->runtime_kernels = (int64_t)c.n_runtime.load();
+    out->own_kernels = (int64_t)c.n_own.load();
     return NVRX_OK;
 }
 

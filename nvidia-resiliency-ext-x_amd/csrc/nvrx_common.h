@@ -193,7 +193,10 @@ __device__ __forceinline__ void lane_sums_f64(const unsigned (&v)[PL], uint64_t&
 #define NVRX_KEY_WIDE_F32BITS 0x4F600000u  // bits of f32(0xE0000000) = 1.75 * 2^31
 #endif
 
-// f32(ns) of a key: the value the reference divides by 1000
+// f32(ns) of a key: the value the reference divides by 1000.  u32 values above NVRX_KEY_MAX
+// (0xF0200000, the key of f32(2^64 - 1)) come from no u64 duration; they continue the same
+// monotone f32 bit pattern (durations beyond 2^64 ns), so selection on keys stays exact for
+// every u32.
 __host__ __device__ __forceinline__ float key_to_f32(unsigned k) {
     return k < NVRX_KEY_WIDE ? (float)k : __builtin_bit_cast(float, k - NVRX_KEY_WIDE + NVRX_KEY_WIDE_F32BITS);
 }

@@ -7,6 +7,10 @@
 
 namespace nvrx {
 
+// longest retained segment the one-workgroup EXACT kernel sorts in LDS (128 KiB of f32); longer
+// rings (up to NVRX_MAX_SEGMENT) sort in device scratch (exact_global_body, segment_kernels.h)
+#define NVRX_LDS_SEGMENT 32768
+
 hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_stride,
                                  int64_t seg_begin, int64_t seg_len, int64_t cap, int mode,
                                  const nvrx_stats_soa& out, uint32_t* col_ref, int64_t ncols,
@@ -15,6 +19,8 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
                                 int64_t nseg, int64_t max_len, int64_t cap, int mode,
                                 bool aligned16, const nvrx_stats_soa& out, uint32_t* col_ref,
                                 int64_t ncols, hipStream_t st);
+
+hipError_t encode_ns_u32(uint32_t* ns, int64_t n, hipStream_t st);
 
 hipError_t kernel_ref(const int32_t* num, const float* med, int64_t R, int64_t K, float* ref,
                       uint32_t* scratch, hipStream_t st);
@@ -82,5 +88,9 @@ int capture_start(nvrx_profiler* p);
 int capture_stop(nvrx_profiler* p);
 int capture_flush();
 void capture_detach(nvrx_profiler* p);
+// mark the calling thread's kernel dispatches as the library's own (not captured) until
+// capture_self_end; false when the capture is off or rocprofiler-sdk cannot mark them
+bool capture_self_begin();
+void capture_self_end();
 
 }  // namespace nvrx

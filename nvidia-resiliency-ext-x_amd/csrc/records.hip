@@ -9,8 +9,10 @@
 // statistic; buckets are still written in push order whenever a slot overflowed.
 //
 // One workgroup of RB_WAVES waves owns one stream; per-slot counters live in LDS:
-//   pass 1: LDS histogram of slots (every wave a contiguous quarter of the stream,
-//           16-byte loads = two records per lane);
+//   pass 1: LDS histogram of slots, 16-byte loads = two records per lane: the head of the
+//           stream (up to RB_WAVES * RB_REGS * 64 pairs) swept by all waves together (wave w
+//           takes every RB_WAVES-th 1 KB step) and held in VGPRs, then each wave's contiguous
+//           chunk of the rest (its head kept in the LDS stash);
 //   scan  : keep_s = min(count_s, cap), bucket starts padded to 16 B (aligned loads
 //           in segment_stats), written to seg_off / seg_len / counts;
 //   pass 2: scatter.  Records of slots that did not overflow take LDS atomic cursors
@@ -34,6 +36,13 @@ __host__ __device__ __forceinline__ int64_t stream_slack(int64_t nslots) {
 __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t, int64_t nslots) {
     return ((rec_off[t] + 3) & ~(int64_t)3) + t * stream_slack(nslots);
 }
+
+// Timing-only ablation builds (tools/build_variant.sh -DNVRX_RB_ABLATE=k; outputs are wrong):
+// 1 = stop after pass 1 + the scans, 2 = also skip the staged copy-out and the tiny statistics
+// after pass 2, 3 = skip only the tiny statistics.  0 (the library): the whole kernel.
+#ifndef NVRX_RB_ABLATE
+#define NVRX_RB_ABLATE 0
+#endif
 
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
 // Slots one bucketing pass counts in LDS; a larger slot table is bucketed in passes over
@@ -268,6 +277,7 @@ void records_bucket_kernel(
         if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
     }
     __syncthreads();
+    if (NVRX_RB_ABLATE == 1) return;
     // positions below stage_lim go to LDS (cold buckets only: an overflowed slot's walk
     // writes to memory directly)
     const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
@@ -328,6 +338,7 @@ void records_bucket_kernel(
         // a chunk that is not pair-aligned (np = 0): its records one by one
         if (!wpairs) for_records(rs, lo, hi, lane, false, place);
     }
+    if (NVRX_RB_ABLATE == 2) return;
     if (stage_lim > 0) {  // the assembled head of the bucket array, in 16-byte stores
         __syncthreads();
         const u32x4* sv = (const u32x4*)stage;
@@ -336,7 +347,7 @@ void records_bucket_kernel(
         // records_stats: the statistics of the staged buckets of <= RB_TINY records, one lane
         // per bucket straight from LDS (lane_stats: computeStats bit for bit, as the ragged
         // lane<8> class does), instead of a later kernel re-reading them through a class list
-        if (tiny.num) {
+        if (tiny.num && NVRX_RB_ABLATE != 3) {
             for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
                 const uint32_t total = cnt[s];
                 const uint32_t keep = keep_of(total);

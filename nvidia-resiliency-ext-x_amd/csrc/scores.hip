@@ -133,6 +133,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
     __shared__ double red[4][6];
     __shared__ int zflag[4];
+    __shared__ bool last;
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int lane = tid & 63;
@@ -241,7 +242,25 @@ __global__ __launch_bounds__(256) void scores_kernel(nvrx_score_args a) {
             if (a.strag_rel) a.strag_rel[r] = sr < a.thr_rel;  // NaN compares false
             if (a.strag_ind) a.strag_ind[r] = si < a.thr_ind;
         }
-        if (errbits && a.err) atomicOr(a.err, errbits);
+        if (!a.done) {
+            if (errbits && a.err) atomicOr(a.err, errbits);
+        } else {
+            if (errbits) atomicOr(&a.done[1], (uint32_t)errbits);
+            __threadfence();  // this row's results (and reads of the reference) come first
+            last = atomicAdd(&a.done[0], 1u) == gridDim.x - 1;
+        }
+    }
+    if (!a.done) return;
+    __syncthreads();
+    if (!last) return;
+    // the last workgroup: every other one has finished reading the column reference
+    __threadfence();
+    for (int64_t i = tid; i < 2 * a.reset_ncols; i += 256)
+        a.reset_col_ref[i] = i < a.reset_ncols ? 0x7F800000u : 0u;
+    if (tid == 0) {
+        const uint32_t e = atomicExch(&a.done[1], 0u);
+        if (a.err) *a.err = (int32_t)e;
+        a.done[0] = 0u;
     }
 }
 

@@ -4,6 +4,7 @@
 #pragma once
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "nvrx_common.h"
@@ -490,7 +491,12 @@ __device__ __forceinline__ LeanOut<PL> lean_core(unsigned (&v)[PL], int n, int m
     const unsigned t0 = (unsigned)((n & 1) ? n / 2 : n / 2 - 1);
     const unsigned t1 = (unsigned)(n / 2);
     unsigned wlo = B, below = 0, d0 = 0, d1 = 0;
-    for (int level = 0;; ++level) {
+    // every level narrows the window by LOGNB bits and shift reaches 0 (an exit) by level
+    // ceil(32 / LOGNB): the bound only makes that explicit, so no wave can spin here (round 3's
+    // gfx950 hang was a loop of this shape with control flow merged into its exits)
+    constexpr int LEVELS = (32 + LOGNB - 1) / LOGNB + 1;
+#pragma unroll 1
+    for (int level = 0; level < LEVELS; ++level) {
         if (level > 0) {
             if (FULL) {
 #pragma unroll
@@ -971,6 +977,138 @@ __global__ __launch_bounds__(256) void seg_stats_exact_kernel(Segs segs, int64_t
 }
 
 // ---------------------------------------------------------------------------
+// Rings longer than the LDS holds (statsMaxLenPerKernel > NVRX_LDS_SEGMENT; the reference's
+// CircularBuffer takes any capacity, CuptiProfiler.h:49-51).  One 1024-thread workgroup per
+// segment sorts its samples in a slice `g` of a device scratch buffer (np2 floats): the bitonic
+// stages whose partner distance j reaches XG_CHUNK run in global memory; for every k the stages
+// below it stay inside aligned XG_CHUNK blocks, which are sorted in LDS.  The sequential f32 sums
+// of computeStats then run on one lane over the sorted samples staged through LDS chunk by
+// chunk -- the same statements, so every field is bit-exact.  Global stores are visible to the
+// block after __syncthreads (one workgroup, one CU).
+// ---------------------------------------------------------------------------
+#define XG_CHUNK 8192
+#define XG_THREADS 1024
+__device__ __forceinline__ void bitonic_step(float* b, int i, int j, int k) {
+    const int ixj = i ^ j;
+    if (ixj > i) {
+        const float a = b[i], c = b[ixj];
+        if (((i & k) == 0) ? (a > c) : (a < c)) {
+            b[i] = c;
+            b[ixj] = a;
+        }
+    }
+}
+
+__device__ __forceinline__ void exact_global_body(const uint32_t* p, int n, int64_t s, float* g,
+                                                  float* lds, const nvrx_stats_soa& out,
+                                                  const ColRef& cr) {
+    int np2 = XG_CHUNK;
+    while (np2 < n) np2 <<= 1;
+    for (int i = threadIdx.x; i < np2; i += XG_THREADS) g[i] = (i < n) ? ns_to_us(p[i]) : __builtin_inff();
+    __syncthreads();
+    // the stages of k <= XG_CHUNK, one aligned chunk at a time in LDS; then, for every larger k,
+    // the global stages (j >= XG_CHUNK) and the remaining ones per chunk in LDS.  The direction
+    // bit (i & k) is taken on the global index.
+    for (int k = 2; k <= np2; k <<= 1) {
+        if (k <= XG_CHUNK && k != 2) continue;  // k = 2 .. XG_CHUNK all run on the first visit
+        const int kmax = k == 2 ? XG_CHUNK : k;
+        int j = k >> 1;
+        if (k > XG_CHUNK) {
+            for (; j >= XG_CHUNK; j >>= 1) {  // partners XG_CHUNK or more apart: global memory
+                for (int i = threadIdx.x; i < np2; i += XG_THREADS) bitonic_step(g, i, j, k);
+                __syncthreads();
+            }
+        }
+        for (int c0 = 0; c0 < np2; c0 += XG_CHUNK) {
+            for (int i = threadIdx.x; i < XG_CHUNK; i += XG_THREADS) lds[i] = g[c0 + i];
+            __syncthreads();
+            for (int kk = k; kk <= kmax; kk <<= 1) {
+                for (int jj = (kk == k ? j : kk >> 1); jj > 0; jj >>= 1) {
+                    for (int i = threadIdx.x; i < XG_CHUNK; i += XG_THREADS) {
+                        const int ixj = i ^ jj;
+                        if (ixj > i) {
+                            const float a = lds[i], c = lds[ixj];
+                            if ((((c0 + i) & kk) == 0) ? (a > c) : (a < c)) {
+                                lds[i] = c;
+                                lds[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            for (int i = threadIdx.x; i < XG_CHUNK; i += XG_THREADS) g[c0 + i] = lds[i];
+            __syncthreads();
+        }
+    }
+    // CuptiProfiler.cpp:53-71, statement by statement; the sums stage the sorted samples in LDS
+    float acc = 0.0f;
+    for (int c0 = 0; c0 < n; c0 += XG_CHUNK) {
+        const int m = min(XG_CHUNK, n - c0);
+        for (int i = threadIdx.x; i < m; i += XG_THREADS) lds[i] = g[c0 + i];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < m; ++i) acc = acc + lds[i];
+        __syncthreads();
+    }
+    const float avg = acc / (float)n;  // meaningful on thread 0 only (the others never summed)
+    float sqs = 0.0f;
+    for (int c0 = 0; c0 < n; c0 += XG_CHUNK) {
+        const int m = min(XG_CHUNK, n - c0);
+        for (int i = threadIdx.x; i < m; i += XG_THREADS) lds[i] = g[c0 + i];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int i = 0; i < m; ++i) {
+                const float t = lds[i] - avg;
+                sqs = sqs + t * t;
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float med = (n % 2 == 0) ? (g[n / 2 - 1] + g[n / 2]) / 2 : g[n / 2];
+        out.num[s] = n;
+        out.min[s] = g[0];
+        out.max[s] = g[n - 1];
+        out.med[s] = med;
+        cr.add(s, med);
+        out.avg[s] = avg;
+        out.std[s] = (float)__builtin_sqrt((double)(sqs / (float)n));
+    }
+    __syncthreads();  // g and lds are reused by the block's next segment
+}
+
+// segments s0 + blockIdx.x (a chunk of the batch: the scratch holds one slice per block)
+template <class Segs>
+__global__ __launch_bounds__(XG_THREADS) void seg_stats_exact_global_kernel(
+    Segs segs, int64_t s0, int64_t nseg, float* work, int64_t np2, nvrx_stats_soa out, ColRef cr) {
+    __shared__ __attribute__((aligned(16))) float lds[XG_CHUNK];
+    const int64_t s = s0 + blockIdx.x;
+    if (s >= nseg) return;
+    const uint32_t* p;
+    int n;
+    segs.get(s, p, n);
+    if (n <= 0) {
+        if (n == 0 && threadIdx.x == 0) {
+            write_empty(out, s);
+            cr.miss(s);
+        }
+        return;
+    }
+    exact_global_body(p, n, s, work + (int64_t)blockIdx.x * np2, lds, out, cr);
+}
+
+// scratch for the global path: np2 floats per block, bounded to ~256 MiB (at least one block)
+static inline int64_t exact_global_np2(int64_t max_len) {
+    int64_t np2 = XG_CHUNK;
+    while (np2 < max_len) np2 <<= 1;
+    return np2;
+}
+static inline int64_t exact_global_blocks(int64_t np2, int64_t want) {
+    const int64_t per = std::max<int64_t>(1, ((int64_t)256 << 20) / (np2 * (int64_t)sizeof(float)));
+    return std::max<int64_t>(1, std::min(want, per));
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launchers shared by segment_stats.hip and segment_ragged.hip
 // ---------------------------------------------------------------------------
 // col_ref: [min med bits | missing] per column, initialised to (+inf, 0) on `st` by one
@@ -981,10 +1119,12 @@ __global__ void colref_init_kernel(uint32_t* col_ref, int64_t ncols) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 2 * ncols) col_ref[i] = i < ncols ? 0x7F800000u : 0u;
 }
-static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream_t st, ColRef& cr) {
+static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream_t st, ColRef& cr,
+                                     bool ready = false) {
     cr = ColRef{nullptr, nullptr, 1, 1.0};
     if (!col_ref || ncols <= 0) return hipSuccess;
     cr = ColRef{col_ref, col_ref + ncols, ncols, 1.0 / (double)ncols};
+    if (ready) return hipSuccess;  // NVRX_STATS_COLREF_READY: initialised by the caller
     hipLaunchKernelGGL(colref_init_kernel<0>, dim3((unsigned)((2 * ncols + 255) / 256)), dim3(256), 0,
                        st, col_ref, ncols);
     return hipGetLastError();
@@ -999,6 +1139,8 @@ static inline hipError_t make_colref(uint32_t* col_ref, int64_t ncols, hipStream
 #ifndef NVRX_LEAN_GROUP_MAX
 #define NVRX_LEAN_GROUP_MAX 8
 #endif
+// one segment's results per lane, wide-key flags in a 64-bit mask
+static_assert(NVRX_LEAN_GROUP_MAX >= 1 && NVRX_LEAN_GROUP_MAX <= 64, "NVRX_LEAN_GROUP_MAX in [1, 64]");
 #ifndef NVRX_LEAN_GROUP_PL_MAX  // FULL segments of up to 64 * this many samples take the group kernel
 #define NVRX_LEAN_GROUP_PL_MAX 128
 #endif
@@ -1058,9 +1200,22 @@ static hipError_t launch_exact(const Segs& segs, int64_t nseg, int64_t max_len,
         hipLaunchKernelGGL((seg_stats_exact_kernel<1024, Segs>), grid, block, 0, st, segs, nseg, out, cr);
     else if (max_len <= 8192)
         hipLaunchKernelGGL((seg_stats_exact_kernel<8192, Segs>), grid, block, 0, st, segs, nseg, out, cr);
-    else if (max_len <= NVRX_MAX_SEGMENT)
-        hipLaunchKernelGGL((seg_stats_exact_kernel<NVRX_MAX_SEGMENT, Segs>), grid, block, 0, st, segs, nseg, out, cr);
-    else
+    else if (max_len <= NVRX_LDS_SEGMENT)
+        hipLaunchKernelGGL((seg_stats_exact_kernel<NVRX_LDS_SEGMENT, Segs>), grid, block, 0, st, segs, nseg, out, cr);
+    else if (max_len <= NVRX_MAX_SEGMENT) {
+        // longer rings: device scratch, the batch in chunks of blocks (one slice each)
+        const int64_t np2 = exact_global_np2(max_len), chunk = exact_global_blocks(np2, nseg);
+        void* work = nullptr;
+        hipError_t e = hipMallocAsync(&work, (size_t)(chunk * np2) * sizeof(float), st);
+        if (e != hipSuccess) return e;
+        for (int64_t s0 = 0; s0 < nseg && e == hipSuccess; s0 += chunk) {
+            hipLaunchKernelGGL((seg_stats_exact_global_kernel<Segs>), dim3((unsigned)std::min(chunk, nseg - s0)),
+                               dim3(XG_THREADS), 0, st, segs, s0, nseg, (float*)work, np2, out, cr);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(work, st);  // on the error path too
+        return e != hipSuccess ? e : f;
+    } else
         return hipErrorInvalidValue;
     return hipGetLastError();
 }

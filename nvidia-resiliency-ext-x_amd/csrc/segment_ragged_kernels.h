@@ -217,6 +217,8 @@ struct ListOcc {  // the prefetch buffer costs PL more VGPRs, the chunk's result
 #define NVRX_LIST_CHUNK 16
 #endif
 constexpr int LIST_CHUNK = NVRX_LIST_CHUNK;
+// results are held one per lane and the wide-key flags in a 32-bit mask
+static_assert(LIST_CHUNK >= 1 && LIST_CHUNK <= 32, "NVRX_LIST_CHUNK must be in [1, 32]");
 
 template <int PL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ListOcc<PL>::W)))
@@ -345,6 +347,22 @@ __global__ __launch_bounds__(256) void seg_stats_exact_list_kernel(RaggedSegs se
     }
 }
 
+// rings longer than NVRX_LDS_SEGMENT: exact_global_body over a per-block slice of device scratch
+__global__ __launch_bounds__(XG_THREADS) void seg_stats_exact_list_global_kernel(
+    RaggedSegs segs, const uint32_t* list, const uint32_t* cls, float* work, int64_t np2,
+    nvrx_stats_soa out) {
+    const ColRef cr{nullptr, nullptr, 1, 1.0};
+    __shared__ __attribute__((aligned(16))) float lds[XG_CHUNK];
+    const uint32_t start = cls[0], cnt = cls[1];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const int64_t s = list[start + i];
+        const uint32_t* p;
+        int n;
+        segs.get(s, p, n);
+        exact_global_body(p, n, s, work + (int64_t)blockIdx.x * np2, lds, out, cr);
+    }
+}
+
 int cu_count() {
     static int cus[64] = {0};
     int dev = 0;
@@ -402,10 +420,20 @@ hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const
     else if (max_len <= 8192)
         hipLaunchKernelGGL((seg_stats_exact_list_kernel<8192>), dim3(cus * 4), dim3(256), 0, st, segs,
                            list, cls, out);
-    else if (max_len <= NVRX_MAX_SEGMENT)
-        hipLaunchKernelGGL((seg_stats_exact_list_kernel<NVRX_MAX_SEGMENT>), dim3(cus), dim3(256), 0,
+    else if (max_len <= NVRX_LDS_SEGMENT)
+        hipLaunchKernelGGL((seg_stats_exact_list_kernel<NVRX_LDS_SEGMENT>), dim3(cus), dim3(256), 0,
                            st, segs, list, cls, out);
-    else
+    else if (max_len <= NVRX_MAX_SEGMENT) {
+        const int64_t np2 = exact_global_np2(max_len), blocks = exact_global_blocks(np2, cus);
+        void* work = nullptr;
+        hipError_t e = scratch_alloc(&work, (size_t)(blocks * np2) * sizeof(float), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(seg_stats_exact_list_global_kernel, dim3((unsigned)blocks), dim3(XG_THREADS),
+                           0, st, segs, list, cls, (float*)work, np2, out);
+        e = hipGetLastError();
+        const hipError_t f = hipFreeAsync(work, st);
+        return e != hipSuccess ? e : f;
+    } else
         return hipErrorInvalidValue;
     return hipSuccess;
 }

@@ -38,8 +38,10 @@ hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_s
                                  int64_t seg_begin, int64_t seg_len, int64_t cap, int mode,
                                  const nvrx_stats_soa& out, uint32_t* col_ref, int64_t ncols,
                                  hipStream_t st) {
+    const bool ready = (mode & NVRX_STATS_COLREF_READY) != 0;
+    mode &= ~NVRX_STATS_COLREF_READY;
     ColRef cr;
-    if (hipError_t e = make_colref(col_ref, ncols, st, cr); e != hipSuccess) return e;
+    if (hipError_t e = make_colref(col_ref, ncols, st, cr, ready); e != hipSuccess) return e;
     if (nseg <= 0) return hipSuccess;
     StridedSegs segs{ns, seg_stride, seg_begin, seg_len, cap};
     const int64_t keep = (cap > 0 && seg_len > cap) ? cap : seg_len;
@@ -50,6 +52,24 @@ hipError_t segment_stats_strided(const uint32_t* ns, int64_t nseg, int64_t seg_s
     if (mode == NVRX_STATS_EXACT || need > 64 * 128) return launch_exact(segs, nseg, keep, out, cr, st);
     // every strided segment has the same length and (aligned) phase
     return launch_fast(segs, nseg, need, aligned ? keep : -1, out, cr, st);
+}
+
+// raw u32 ns (durations below 2^32 ns, never encoded) -> duration keys, in place: values from
+// NVRX_KEY_WIDE (3.76 s) up become 0xE0000000 + bits(f32(ns)) - bits(f32(0xE0000000)), as
+// nvrx_duration_key encodes the same u64 (v_cvt_f32_u32 rounds to nearest even, like the u64
+// conversion of CuptiProfiler.cpp:187).  One coalesced read-modify-write pass.
+__global__ __launch_bounds__(256) void encode_ns_u32_kernel(uint32_t* ns, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint32_t v = ns[i];
+        if (v >= NVRX_KEY_WIDE) ns[i] = NVRX_KEY_WIDE + (__float_as_uint((float)v) - NVRX_KEY_WIDE_F32BITS);
+    }
+}
+
+hipError_t encode_ns_u32(uint32_t* ns, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(encode_ns_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ns, n);
+    return hipGetLastError();
 }
 
 }  // namespace nvrx

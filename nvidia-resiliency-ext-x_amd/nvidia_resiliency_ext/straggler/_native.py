@@ -13,7 +13,7 @@ import threading
 from typing import Optional
 
 LIB_NAME = "libnvrx_hip.so"
-ABI_VERSION = 3  # include/nvrx_straggler.h NVRX_ABI_VERSION
+ABI_VERSION = 4  # include/nvrx_straggler.h NVRX_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 NVRX_OK = 0
@@ -25,7 +25,8 @@ NVRX_ERR_NOMEM = -5
 
 NVRX_STATS_FAST = 0
 NVRX_STATS_EXACT = 1
-NVRX_MAX_SEGMENT = 32768
+NVRX_STATS_COLREF_READY = 0x10
+NVRX_MAX_SEGMENT = 1 << 30  # rings above 32,768 samples sort in device scratch
 
 P = ctypes.c_void_p
 i32 = ctypes.c_int32
@@ -47,6 +48,7 @@ class ScoreArgs(ctypes.Structure):
         ("partials", P), ("err", P),
         ("round_f32", i32), ("thr_rel", f64), ("thr_ind", f64),
         ("gpu_rel", P), ("gpu_ind", P), ("strag_rel", P), ("strag_ind", P),
+        ("done", P), ("reset_col_ref", P), ("reset_ncols", i64),
     ]
 
 
@@ -56,7 +58,8 @@ class Record(ctypes.Structure):
 
 class CaptureCounters(ctypes.Structure):
     _fields_ = [("callbacks", i64), ("headers", i64), ("dispatches", i64),
-                ("callback_ns", i64), ("flushes", i64), ("flush_ns", i64)]
+                ("callback_ns", i64), ("flushes", i64), ("flush_ns", i64), ("runtime_kernels", i64),
+                ("own_kernels", i64)]
 
 
 class ProfilerConfig(ctypes.Structure):
@@ -72,6 +75,7 @@ SIGNATURES = {
     "nvrx_capture_configure": (ctypes.c_int, []),
     "nvrx_abi_version": (ctypes.c_int, []),
     "nvrx_duration_key": (u32, [ctypes.c_uint64]),
+    "nvrx_encode_ns_u32": (ctypes.c_int, [P, i64, P]),
     "nvrx_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "nvrx_sync": (ctypes.c_int, [P]),
     "nvrx_segment_stats_strided": (ctypes.c_int, [P, i64, i64, i64, i64, i64, i32,
@@ -174,6 +178,7 @@ def stream_handle(stream=None) -> Optional[int]:
 
 KEY_WIDE = 0xE0000000
 KEY_WIDE_F32BITS = 0x4F600000
+KEY_MAX = 0xF0200000  # key of f32(2^64 - 1); larger u32 values come from no u64 duration
 
 
 def duration_keys(ns):

@@ -1,7 +1,8 @@
 """Batched scoring of many (simulated) ranks resident in HBM -- the hot path at scale.
 
 ``MatrixReporter`` runs the whole report for R ranks x K kernels in one pass over a
-uint32 ns matrix ``[R][K][S_push]`` (the last ``cap`` samples of every (rank, kernel)
+u32 duration-key matrix ``[R][K][S_push]`` (``_native.duration_keys``: the integer ns below
+3.76 s; raw u32 ns reaching 3.76 s must go through ``ops.encode_ns_u32_`` first) (the last ``cap`` samples of every (rank, kernel)
 retained, as the reference's per-kernel rings keep them), or over R push-ordered record
 streams ``{slot, ns}`` (``compute_stats_records``: bucket by slot keeping the last ``cap``
 of each, then length-classed segment statistics -- configs[3]):
@@ -104,6 +105,11 @@ class MatrixReporter:
                           gpu_ind=self.out[8 * R:16 * R].view(torch.float64),
                           strag_rel=self.out[16 * R:17 * R], strag_ind=self.out[17 * R:18 * R])
         self.err = self.out[self._e:self._e + 4].view(torch.int32)
+        # self-resetting scores epilogue (nvrx_score_args.done): the scores kernel's last
+        # workgroup stores the error bits and re-initialises col_ref for the next report, so a
+        # report is two launches (statistics, scores) with no initialising fill in between
+        self.done = torch.zeros(2, dtype=torch.int32, device=d)
+        self._colref_clean = False  # col_ref holds the initial reference (set by the epilogue)
 
     def reset_history(self):
         if self.hist is not None:
@@ -120,10 +126,13 @@ class MatrixReporter:
             ops.kernel_ref(st.num, st.med, ref=self._ref_f32, scratch=self.col_ref)
 
     def compute_stats(self, ns: torch.Tensor, s_push: int) -> ops.SegmentStats:
+        # (inside a graph capture the flag describes the device state when the graph replays:
+        # the captured sequences always pair a statistics call with the scores that follow)
         st = ops.segment_stats_strided(ns.view(-1), self.R * self.K, s_push, 0, s_push,
                                        cap=self.cap, mode=self.mode, out=self.stats,
                                        col_ref=self.col_ref if self._fuse_ref() else None,
-                                       ncols=self.K)
+                                       ncols=self.K, colref_ready=self._colref_clean)
+        self._colref_clean = False
         self._column_ref()
         return st
 
@@ -141,6 +150,7 @@ class MatrixReporter:
                  torch.empty(self.R * self.K, dtype=torch.int32, device=d))
             self._bucket = b
         max_len = min(self.cap, n) if self.cap > 0 else n
+        self._colref_clean = False
         return ops.records_stats(recs, rec_off, self.K, self.cap, max(max_len, 1), mode=self.mode,
                                  out=self.stats, bucket=b,
                                  col_ref=self.col_ref if self.relative else None)
@@ -151,29 +161,45 @@ class MatrixReporter:
         self.compute_scores()
         return self.land()
 
-    def _outputs(self):
-        v = self.views
-        return dict(gpu_rel=v["gpu_rel"] if self.relative else None,
-                    gpu_ind=v["gpu_ind"] if self.individual else None,
-                    strag_rel=v["strag_rel"] if self.relative else None,
-                    strag_ind=v["strag_ind"] if self.individual else None,
+    def _outputs(self, buf: Optional[torch.Tensor] = None):
+        R = self.R
+        b = self.out if buf is None else buf
+        return dict(gpu_rel=b[0:8 * R].view(torch.float64) if self.relative else None,
+                    gpu_ind=b[8 * R:16 * R].view(torch.float64) if self.individual else None,
+                    strag_rel=b[16 * R:17 * R] if self.relative else None,
+                    strag_ind=b[17 * R:18 * R] if self.individual else None,
                     thr_rel=self.thr_rel, thr_ind=self.thr_ind, round_f32=self.round_f32)
 
-    def compute_scores(self) -> None:
-        """Scores + straggler masks into the packed device buffer (one kernel on 1 GPU;
-        partials -> RCCL all_gather -> finalize on N GPUs)."""
+    def compute_scores(self, out_buf: Optional[torch.Tensor] = None) -> None:
+        """Scores + straggler masks into the packed buffer (one kernel on 1 GPU; partials ->
+        RCCL all_gather -> finalize on N GPUs).  out_buf: another packed buffer of the same
+        layout (1 GPU), e.g. pinned host memory the kernel writes directly (no copy)."""
         R, K = self.R, self.K
         st = self.stats.view(R, K)
-        self.err.zero_()
         ref = self.col_ref.view(torch.float32)[:K] if self.relative else None
         missing = self.col_ref[K:2 * K] if self.relative else None
+        # the self-resetting epilogue where the per-kernel reference is fused into the
+        # statistics (R <= FUSED_REF_MAX_ROWS): one completion counter per report, whose
+        # same-address atomics would cost ~0.15 / 1 ms at 4,096 / 16,384 rows
+        fused = self._fuse_ref()
+        reset = self.col_ref[:2 * K] if fused else None
+        done = self.done if fused else None
         if not self.exchange:
+            b = self.out if out_buf is None else out_buf
+            err = b[self._e:self._e + 4].view(torch.int32)
+            if not fused:
+                err.zero_()
             ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
-                       ref_missing=missing, hist=self.hist, err=self.err,
-                       finalize=self._outputs())
+                       ref_missing=missing, hist=self.hist, err=err,
+                       finalize=self._outputs(b), done=done, reset_col_ref=reset)
+            self._colref_clean = fused
             return
+        if not fused:
+            self.err.zero_()
         ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
-                   ref_missing=missing, hist=self.hist, partials=self.partials, err=self.err)
+                   ref_missing=missing, hist=self.hist, partials=self.partials, err=self.err,
+                   done=done, reset_col_ref=reset)
+        self._colref_clean = fused
         flat = self.gathered.view(self.world * R, 6)
         if self.gloo:  # gloo collectives take host tensors
             hg = torch.empty((self.world * R, 6), dtype=torch.float64)
@@ -231,14 +257,7 @@ class ReportGraph:
 
     def __init__(self, rep: MatrixReporter, ns: torch.Tensor, s_push: int):
         self.rep = rep
-        side = torch.cuda.Stream(rep.device)
-        side.wait_stream(torch.cuda.current_stream(rep.device))
-        with torch.cuda.stream(side):  # one eager pass: first-launch setup outside the capture
-            rep.compute_stats(ns, s_push)
-            if not rep.exchange:
-                rep.compute_scores()
-        torch.cuda.current_stream(rep.device).wait_stream(side)
-        torch.cuda.synchronize(rep.device)
+        _warm_up(rep, ns, s_push)
         self.stats = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.stats):
             rep.compute_stats(ns, s_push)
@@ -275,6 +294,32 @@ class ReportGraph:
         return self.rep._unpack()
 
 
+def _warm_up(rep: MatrixReporter, ns: torch.Tensor, s_push: int) -> None:
+    """One eager report on a side stream (first-launch setup outside any graph capture).  The
+    individual history is restored afterwards: the warm-up must not fold whatever `ns` holds
+    now into it (the graphs' reports advance it exactly as report() does)."""
+    d = rep.device
+    saved = rep.hist.clone() if rep.hist is not None else None
+    side = torch.cuda.Stream(d)
+    side.wait_stream(torch.cuda.current_stream(d))
+    with torch.cuda.stream(side):
+        rep.compute_stats(ns, s_push)
+        if not rep.exchange:
+            rep.compute_scores()
+        elif rep._fuse_ref():  # N GPUs: leave col_ref initialised without the exchange
+            rep.col_ref[:rep.K].fill_(0x7F800000)
+            rep.col_ref[rep.K:2 * rep.K].zero_()
+            rep._colref_clean = True
+        if saved is not None:
+            rep.hist.copy_(saved)
+    torch.cuda.current_stream(d).wait_stream(side)
+    torch.cuda.synchronize(d)
+
+
+# NVRX_PIPE_D2H=copy: pipelined reports write a device buffer and copy it to the pinned one
+# (one more graph node) instead of the scores kernel writing pinned host memory directly
+_PIPE_COPY = os.environ.get("NVRX_PIPE_D2H", "") == "copy"
+
 TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
 
 
@@ -294,15 +339,8 @@ class PipelinedReports:
         if rep.exchange:
             raise RuntimeError("pipelined reports: 1 GPU (the partials exchange is an eager collective)")
         self.rep, self.timing = rep, timing
-        d = rep.device
-        side = torch.cuda.Stream(d)
-        side.wait_stream(torch.cuda.current_stream(d))
-        with torch.cuda.stream(side):  # one eager pass: first-launch setup outside the capture
-            rep.compute_stats(ns, s_push)
-            rep.compute_scores()
-        torch.cuda.current_stream(d).wait_stream(side)
-        torch.cuda.synchronize(d)
-        self.bufs = [torch.empty_like(rep.h_out, pin_memory=True) for _ in range(2)]
+        _warm_up(rep, ns, s_push)
+        self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
 
         def capture(stats: bool, rest: bool, k: int):
             g = torch.cuda.CUDAGraph()
@@ -310,8 +348,14 @@ class PipelinedReports:
                 if stats:
                     rep.compute_stats(ns, s_push)
                 if rest:
-                    rep.compute_scores()
-                    self.bufs[k].copy_(rep.out, non_blocking=True)
+                    # the scores kernel writes the pinned buffer itself when its epilogue stores
+                    # the error word (fused reference, R <= FUSED_REF_MAX_ROWS); otherwise the
+                    # error word is zeroed on the device first and the results copied
+                    if _PIPE_COPY or not rep._fuse_ref():
+                        rep.compute_scores()
+                        self.bufs[k].copy_(rep.out, non_blocking=True)
+                    else:  # the scores kernel writes the pinned buffer itself
+                        rep.compute_scores(out_buf=self.bufs[k])
             return g
 
         self.full = [capture(True, True, k) for k in range(2)]

@@ -55,12 +55,14 @@ def _stream(stream):
 def segment_stats_strided(ns: torch.Tensor, nseg: int, seg_stride: int, seg_begin: int,
                           seg_len: int, cap: int = 0, mode: int = STATS_FAST,
                           out: Optional[SegmentStats] = None, col_ref: Optional[torch.Tensor] = None,
-                          ncols: int = 0, stream=None) -> SegmentStats:
-    """Stats of segments ns.flat[s*seg_stride + seg_begin : +seg_len] (uint32 ns), last
+                          ncols: int = 0, stream=None, colref_ready: bool = False) -> SegmentStats:
+    """Stats of segments ns.flat[s*seg_stride + seg_begin : +seg_len] (u32 duration keys,
+    ``_native.duration_keys``: plain ns below 3.76 s -- raw u32 ns of 3.76 s and more need
+    ``encode_ns_u32_`` first; a u32 above ``_native.KEY_MAX`` comes from no u64 duration), last
     `cap` samples retained (CircularBuffer.h:53-69).  reference: CuptiProfiler.cpp:44-74."""
     N.require_device(ns, "ns")
     if ns.dtype not in (torch.int32, torch.uint32):
-        raise TypeError("ns must be a 32-bit integer tensor of nanosecond durations")
+        raise TypeError("ns must be a 32-bit integer tensor of duration keys")
     if nseg > 0 and (nseg - 1) * seg_stride + seg_begin + seg_len > ns.numel():
         raise ValueError("segments exceed the ns tensor")
     if out is None:
@@ -68,9 +70,22 @@ def segment_stats_strided(ns: torch.Tensor, nseg: int, seg_stride: int, seg_begi
     soa = out.soa()
     if col_ref is not None and (col_ref.numel() < 2 * ncols or col_ref.dtype != torch.int32):
         raise ValueError("col_ref must be an int32 tensor of >= 2*ncols elements")
+    if colref_ready:  # col_ref holds the initial reference already (a previous scores epilogue)
+        mode |= N.NVRX_STATS_COLREF_READY
     N.call("nvrx_segment_stats_strided", ns.data_ptr(), nseg, seg_stride, seg_begin, seg_len,
            cap, mode, ctypes.byref(soa), N.ptr(col_ref), ncols, _stream(stream))
     return out
+
+
+def encode_ns_u32_(ns: torch.Tensor, stream=None) -> torch.Tensor:
+    """In place: raw u32 integer-ns durations (any value below 2^32, never encoded) -> duration
+    keys.  Values below 3.76 s are unchanged; from 3.76 s up they become the key of f32(ns), the
+    value CuptiProfiler.cpp:187 keeps.  Not idempotent: encode raw ns once."""
+    N.require_device(ns, "ns")
+    if ns.dtype not in (torch.int32, torch.uint32) or not ns.is_contiguous():
+        raise TypeError("ns must be a contiguous 32-bit integer tensor")
+    N.call("nvrx_encode_ns_u32", ns.data_ptr(), ns.numel(), _stream(stream))
+    return ns
 
 
 def segment_stats_ragged(ns: torch.Tensor, seg_off: torch.Tensor, seg_len: Optional[torch.Tensor],
@@ -118,10 +133,13 @@ def pack_min_times(med: torch.Tensor, ids: torch.Tensor, total: int,
 
 def scores(num, med, avg, *, col_valid=None, ref=None, ref_index=None, ref_missing=None,
            hist=None, hist_index=None, hist_stride=0, partials=None, err=None,
-           finalize: Optional[dict] = None, stream=None):
+           finalize: Optional[dict] = None, done=None, reset_col_ref=None, stream=None):
     """Per-row partial sums {sum s*w, sum w, n} for rel and indiv (reporting.py:219-253).
     finalize = dict(gpu_rel=, gpu_ind=, strag_rel=, strag_ind=, thr_rel=, thr_ind=,
-    round_f32=) finishes the scores in the same kernel (single shard)."""
+    round_f32=) finishes the scores in the same kernel (single shard).  done (2 int32, zero
+    before the first call): self-resetting epilogue -- err is stored, not OR-ed (no zeroing
+    needed), and reset_col_ref ([2*K'] int32) is re-initialised for the next statistics call
+    (segment_stats_strided(colref_ready=True))."""
     R, K = med.shape
     if partials is None and finalize is None:
         partials = torch.empty((R, 6), dtype=torch.float64, device=med.device)
@@ -134,7 +152,9 @@ def scores(num, med, avg, *, col_valid=None, ref=None, ref_index=None, ref_missi
                     N.ptr(hist), N.ptr(hist_index), hist_stride, N.ptr(partials), N.ptr(err),
                     int(fz.get("round_f32", False)), float(fz.get("thr_rel", 0.75)),
                     float(fz.get("thr_ind", 0.75)), N.ptr(fz.get("gpu_rel")),
-                    N.ptr(fz.get("gpu_ind")), N.ptr(fz.get("strag_rel")), N.ptr(fz.get("strag_ind")))
+                    N.ptr(fz.get("gpu_ind")), N.ptr(fz.get("strag_rel")), N.ptr(fz.get("strag_ind")),
+                    N.ptr(done), N.ptr(reset_col_ref),
+                    reset_col_ref.numel() // 2 if reset_col_ref is not None else 0)
     N.call("nvrx_scores", ctypes.byref(a), _stream(stream))
     return partials
 

@@ -20,7 +20,7 @@ def key_values(keys):
         return O.key_to_f32(k).astype(np.float64)
     return k.astype(np.float64)
 STD_RTOL = 1e-6
-LANE_EXACT = 16
+LANE_EXACT = 128  # the lane classes (<= 128 records, nvrx_straggler.h) are bit-exact
 
 
 def check_avg_std(g_avg, g_std, ref, xmean, xstd, tag=""):

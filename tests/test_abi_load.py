@@ -31,7 +31,7 @@ def test_python_binding_covers_header():
 
 def test_lib_loads_and_reports_abi():
     L = _native.lib()
-    assert L.nvrx_abi_version() == _native.ABI_VERSION == 3
+    assert L.nvrx_abi_version() == _native.ABI_VERSION == 4
     cnt = ctypes.c_int(-1)
     # no HIP device in the CPU container: the call succeeds (0 devices) or reports HIP error
     rc = L.nvrx_device_count(ctypes.byref(cnt))

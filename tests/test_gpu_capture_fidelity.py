@@ -186,3 +186,116 @@ def test_drain_at_stop_and_destroy_while_delivering():
     assert out["num"].get(key) == 5000, out["num"]
     assert not [k for k in out["keys"] if "rocclr" in k], out["keys"]  # nothing of our own
     assert out["after"] == {key: 10}
+
+
+PROBE = os.path.join(ROOT, "tests", "native", "grid_probe.hsaco")
+
+RUNTIME = r"""
+import ctypes, json, os
+from nvidia_resiliency_ext.straggler import cupti, ops, _native
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=1024, capture=True)
+p.initialize()
+hip = ctypes.CDLL("libamdhip64.so")
+src = torch.rand(1 << 20, device="cuda")
+dst = torch.empty_like(src)
+score = torch.rand(1000, dtype=torch.float64, device="cuda")
+m = torch.empty(1000, dtype=torch.uint8, device="cuda")
+buf = torch.zeros(1024, dtype=torch.int32, device="cuda")
+mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+assert hip.hipModuleLoad(ctypes.byref(mod), PROBE.encode()) == 0
+assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"nvrx_grid_probe") == 0
+stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+a_out, a_n = ctypes.c_void_p(buf.data_ptr()), ctypes.c_uint32(1000)
+params = (ctypes.c_void_p * 2)(ctypes.cast(ctypes.byref(a_out), ctypes.c_void_p),
+                               ctypes.cast(ctypes.byref(a_n), ctypes.c_void_p))
+hip.hipExtModuleLaunchKernel.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [
+    ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+    ctypes.c_void_p, ctypes.c_uint32]
+hip.hipMemsetAsync.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p]
+def section():
+    dst.copy_(src)  # same device, contiguous: hipMemcpyAsync D2D (a runtime blit kernel)
+    rc = hip.hipMemsetAsync(ctypes.c_void_p(dst.data_ptr()), 0, dst.numel() * 4, stream)
+    assert rc == 0, ("hipMemsetAsync", rc)
+    ops.stragglers(score, 0.5, out=m)  # the one real kernel: 256 threads, 4 blocks
+    # global size 1000 over workgroups of 256: a partial last block, 4 blocks as CUPTI counts
+    rc = hip.hipExtModuleLaunchKernel(fn, 1000, 1, 1, 256, 1, 1, 0, stream, params, None,
+                                      None, None, 0)
+    assert rc == 0, ("hipExtModuleLaunchKernel", rc)
+section()  # warm-up, stopped: nothing recorded
+torch.cuda.synchronize()
+c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
+p.start()
+for _ in range(3):
+    section()
+torch.cuda.synchronize()
+stats = {k: v.num_calls for k, v in p.get_stats().items()}
+c1 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c1))
+p.stop()
+p.shutdown()
+assert buf[:1000].tolist() == list(range(1000))
+print("RESULT " + json.dumps({"stats": stats, "available": cupti.capture_available(),
+                              "runtime": c1.runtime_kernels - c0.runtime_kernels}))
+""".replace("PROBE", repr(PROBE))
+
+
+def test_runtime_copies_and_fills_are_not_kernels_and_partial_blocks_count():
+    """CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL only (CuptiProfiler.cpp:118, 179): a section of
+    copy_ + hipMemsetAsync + two kernels yields exactly the two kernels' keys; gridX counts the
+    partial last block of a global size of 1000 over 256-wide workgroups (:182-185)."""
+    assert os.path.exists(PROBE), "build tests/native first (__graft_entry__.build())"
+    out = _child(RUNTIME)
+    assert out["available"]
+    assert out["stats"] == {f"{STRAG}_blk_256_1_1_grid_4_1_1": 3,
+                            "nvrx_grid_probe_blk_256_1_1_grid_4_1_1": 3}, out["stats"]
+    assert out["runtime"] >= 6, out  # the copies and fills were dispatched, and left out
+    kept = _child(RUNTIME, env={"NVRX_CAPTURE_RUNTIME_KERNELS": "1"})
+    blits = {k: n for k, n in kept["stats"].items() if k.startswith("__amd_rocclr_")}
+    assert blits and sum(blits.values()) >= 6, kept["stats"]
+    assert kept["runtime"] == 0
+
+
+CONCURRENT = r"""
+import ctypes, json, threading
+from nvidia_resiliency_ext.straggler import cupti, ops, _native
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=8192, capture=True)
+p.initialize()
+score = torch.rand(1000, dtype=torch.float64, device="cuda")
+m = torch.empty(1000, dtype=torch.uint8, device="cuda")
+ops.stragglers(score, 0.5, out=m)
+torch.cuda.synchronize()
+c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
+p.start()
+N = 3000
+go = threading.Event()
+def launcher():
+    go.wait()
+    for i in range(N):
+        ops.stragglers(score, 0.5, out=m)
+    torch.cuda.synchronize()
+t = threading.Thread(target=launcher)
+t.start()
+go.set()
+reports = 0
+while t.is_alive():  # reports while the other thread launches (its kernels must all count)
+    p.get_stats()
+    reports += 1
+t.join()
+torch.cuda.synchronize()
+stats = {k: v.num_calls for k, v in p.get_stats().items()}
+c1 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c1))
+p.stop()
+p.shutdown()
+print("RESULT " + json.dumps({"stats": stats, "reports": reports,
+                              "own": c1.own_kernels - c0.own_kernels}))
+"""
+
+
+def test_reports_leave_out_their_own_kernels_but_not_other_threads():
+    """get_stats runs HIP kernels; they are not the job's (the reference's getStats is host code)
+    and are left out by thread, so kernels another thread launches DURING the reports are all
+    captured (CUPTI stays enabled through getStats, CuptiProfiler.cpp:136-146)."""
+    out = _child(CONCURRENT)
+    assert out["stats"] == {f"{STRAG}_blk_256_1_1_grid_4_1_1": 3000}, out
+    assert out["reports"] >= 2 and out["own"] > 0, out

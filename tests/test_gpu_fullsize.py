@@ -152,7 +152,7 @@ def test_config3_full_world():
         g = _stats_host(rep)
         h = recs.cpu().numpy().view(np.uint32)
         ref = O.records_stats(h, h_off, K, cap=cap, nthreads=THREADS)
-        # AVG / STD of EVERY bucket: bit-exact for <= 16 records, else within the FAST bars of
+        # AVG / STD of EVERY bucket: bit-exact for <= 128 records, else within the FAST bars of
         # the exact moments (segments of > 128 samples included)
         xm, xs = O.records_moments(h, h_off, K, cap=cap, nthreads=THREADS)
         del h
@@ -167,7 +167,7 @@ def test_config3_full_world():
     b = _stats_host(rep2)
     for f in EXACT_FIELDS:
         assert np.array_equal(g[f].view(np.uint32), b[f].view(np.uint32)), f
-    short = g["num"] <= 16
+    short = g["num"] <= 128  # lane classes: bit-exact whatever the push order
     for f in ("avg", "std"):
         assert np.array_equal(g[f][short].view(np.uint32), b[f][short].view(np.uint32)), f
         np.testing.assert_allclose(b[f], g[f], rtol=2.5e-7, atol=0)

@@ -180,12 +180,10 @@ def test_cupti_manager_refcount():
         m.shutdown()
 
 
-# FAST mode with 0 < cap <= the LDS stage runs records_resident.hip (one pass, buckets never
-# written); cap 0 / EXACT / too many slots for its LDS run records_bucket + the ragged classes.
-# (52, 8192, 900, 1100): ~52k records per stream, past the 48,128 a workgroup holds in VGPRs
-# (its records re-read from memory at every pass); (500, 100, ...): rings overflow in several
-# LDS groups; (6000, 100, ...): the resident kernel's largest slot tables; (9000, 8192, ...): a
-# stage too small for the ring (bucketing path)
+# records_bucket (records.hip) + the length-classed ragged kernels.  (52, 8192, 900, 1100): ~52k
+# records per stream, past the 16,384 pairs a workgroup holds in VGPRs and its LDS stash, so
+# pass 2 re-reads from memory; (500, 100, ...): overflowed rings; (6000, 100, ...) / (9000, 8192,
+# ...): large slot tables, whose buckets do not all fit the LDS stage
 @pytest.mark.parametrize("nslots,cap,lo,hi", [(37, 8192, 0, 40), (37, 5, 0, 30), (3000, 0, 0, 3),
                                               (500, 100, 0, 150), (64, 8192, 60, 70),
                                               (52, 8192, 900, 1100), (6000, 100, 0, 6),
@@ -209,8 +207,8 @@ def test_records_stats_fused_matches_oracle(nslots, cap, lo, hi):
     ref = O.records_stats(recs, off.astype(np.int64), nslots, cap=cap, nthreads=4)
     for f in ("num", "min", "max", "med"):
         assert np.array_equal(getattr(st, f).numpy().view(np.int32), ref[f].view(np.int32)), f
-    # AVG / STD: bit-exact for <= 16 records, else bit-exact or within the FAST bars of the
-    # exact moments (2.5e-7 / 1e-6)
+    # AVG / STD: bit-exact for <= 128 records (lane classes), else bit-exact or within the FAST
+    # bars of the exact moments (2.5e-7 / 1e-6)
     xm, xs = O.records_moments(recs, off.astype(np.int64), nslots, cap=cap, nthreads=4)
     check_avg_std(st.avg.numpy(), st.std.numpy(), ref, xm, xs, f"nslots={nslots} cap={cap}")
     num = ref["num"].reshape(nstreams, nslots)
@@ -370,8 +368,8 @@ def test_profiler_durations_of_any_length(exact):
 
 @pytest.mark.parametrize("n", [5, 40, 3000])
 def test_records_stats_wide_keys(n):
-    # FAST record statistics (records_resident.hip: lane path <= 16 records, wave path above)
-    # over buckets mixing narrow and wide duration keys: MIN/MAX/MED bit-exact with the
+    # FAST record statistics (records_bucket + ragged classes: lane classes <= 128 records, wave
+    # classes above) over buckets mixing narrow and wide duration keys: MIN/MAX/MED bit-exact with the
     # reference's floats, AVG/STD within the FAST bars of the decoded values' moments
     rng = np.random.default_rng(n)
     nslots, nstreams = 3, 2
@@ -393,8 +391,9 @@ def test_records_stats_wide_keys(n):
         assert st.num[g].item() == n
         got = [np.float32(getattr(st, f)[g].item()) for f in ("min", "max", "med")]
         assert got == [np.float32(ref.min), np.float32(ref.max), np.float32(ref.median)], (g, s)
-        if n <= 16:
-            assert np.float32(st.avg[g].item()) == np.float32(ref.avg)
+        if n <= 128:  # lane classes: computeStats' own sequential f32 sums
+            assert (np.float32(st.avg[g].item()), np.float32(st.std[g].item())) == \
+                (np.float32(ref.avg), np.float32(ref.stddev))
         else:
             v = O.key_to_f32(O.duration_key(ns)).astype(np.float64) if s != 1 else ns.astype(np.float64)
             np.testing.assert_allclose(st.avg[g].item(), v.mean() / 1000, rtol=2.5e-7)
@@ -485,3 +484,156 @@ def test_records_streams_around_the_register_head(cap):
         assert np.array_equal(getattr(st, f).numpy().view(np.int32), ref[f].view(np.int32)), f
     xm, xs = O.records_moments(recs, off, nslots, cap=cap, nthreads=4)
     check_avg_std(st.avg.numpy(), st.std.numpy(), ref, xm, xs, f"register head cap={cap}")
+
+
+def _wide_kat():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "compute_stats_wide_kat.json")) as f:
+        return json.load(f)
+
+
+def _bits(x):
+    return int(np.float32(x).view(np.uint32))
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_wide_duration_kat_through_profiler(exact):
+    """u64 durations of 2^32 ns and more, against the REFERENCE-generated
+    fixture (compute_stats_wide_kat.json: ref_ns_to_us + computeStats of the reference build).
+    EXACT: every field bit-exact.  FAST: NUM/MIN/MAX/MED bit-exact, AVG/STD bit-exact for rings
+    of <= 128 (lane classes), else within the FAST bars of the decoded values' exact moments."""
+    kat = _wide_kat()
+    for cap in sorted({c["cap"] for c in kat["cases"]}):
+        cases = [c for c in kat["cases"] if c["cap"] == cap]
+        p = cupti.KernelProfiler(statsMaxLenPerKernel=cap, exact=exact)
+        try:
+            p.initialize()
+            p.start()
+            for c in cases:
+                p.push(c["name"] + "_blk_1_1_1_grid_1_1_1", np.array(c["ns"], np.uint64))
+            st = p.get_stats()
+            for c in cases:
+                s = st[c["name"] + "_blk_1_1_1_grid_1_1_1"]
+                got = [s.num_calls] + [_bits(v) for v in (s.min, s.max, s.median, s.avg, s.stddev)]
+                e = c["expect"]
+                if exact or e[0] <= 128:
+                    assert got == e, c["name"]
+                else:
+                    assert got[:4] == e[:4], c["name"]
+                    v = O.key_to_f32(O.duration_key(np.array(c["ns"], np.uint64)[-cap:])).astype(np.float64)
+                    np.testing.assert_allclose(s.avg, v.mean() / 1000, rtol=2.5e-7)
+                    np.testing.assert_allclose(s.stddev, v.std() / 1000, rtol=1e-6)
+        finally:
+            p.close()
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_EXACT, ops.STATS_FAST])
+def test_wide_duration_kat_through_matrix_segments(mode):
+    """The same fixture through segment_stats_ragged on duration keys (one segment per case of
+    cap 8192; the ring retention of a segment is its last `cap` keys)."""
+    kat = _wide_kat()
+    cases = [c for c in kat["cases"] if c["cap"] == 8192]
+    keys = [O.duration_key(np.array(c["ns"], np.uint64)) for c in cases]
+    off = np.zeros(len(keys) + 1, np.int64)
+    off[1:] = np.cumsum([k.size for k in keys])
+    d = torch.from_numpy(np.concatenate(keys).view(np.int32)).cuda()
+    st = ops.segment_stats_ragged(d, torch.from_numpy(off).cuda(), None, int(max(k.size for k in keys)),
+                                  cap=8192, mode=mode).cpu()
+    for i, c in enumerate(cases):
+        got = [int(st.num[i])] + [_bits(getattr(st, f)[i].item()) for f in ("min", "max", "med", "avg", "std")]
+        e = c["expect"]
+        if mode == ops.STATS_EXACT or e[0] <= 128:
+            assert got == e, c["name"]
+        else:
+            assert got[:4] == e[:4], c["name"]
+            v = O.key_to_f32(keys[i]).astype(np.float64)
+            np.testing.assert_allclose(st.avg[i].item(), v.mean() / 1000, rtol=2.5e-7)
+            np.testing.assert_allclose(st.std[i].item(), v.std() / 1000, rtol=1e-6)
+
+
+def test_raw_u32_ns_need_encoding():
+    """a raw u32 ns of 3.76 s or more is not a duration key.  encode_ns_u32_ turns raw
+    ns into keys on the device, after which the reference's f32(ns) / 1000 of a 4.0 s kernel
+    comes out bit for bit."""
+    raw = np.array([1000, 2000, 4_000_000_000, 3_900_000_123, 4_294_967_295, 3_758_096_384, 7],
+                   np.uint32)
+    t = torch.from_numpy(raw.view(np.int32).copy()).cuda()
+    ops.encode_ns_u32_(t)
+    enc = t.cpu().numpy().view(np.uint32)
+    assert np.array_equal(enc, O.duration_key(raw.astype(np.uint64)))
+    for mode in (ops.STATS_FAST, ops.STATS_EXACT):
+        st = ops.segment_stats_strided(t, 1, raw.size, 0, raw.size, mode=mode).cpu()
+        ref = O.compute_stats(O.ns_to_us(raw.astype(np.uint64)))
+        assert [_bits(getattr(st, f)[0].item()) for f in ("min", "max", "med")] == \
+            [_bits(ref.min), _bits(ref.max), _bits(ref.median)]
+        assert np.float32(st.max[0].item()) == np.float32(np.float32(4_294_967_295) / np.float32(1000))
+    # a larger encoded array: the grid-stride loop, every element
+    big = np.random.default_rng(3).integers(0, 2**32, size=1_000_003, dtype=np.uint64).astype(np.uint32)
+    tb = torch.from_numpy(big.view(np.int32).copy()).cuda()
+    assert np.array_equal(ops.encode_ns_u32_(tb).cpu().numpy().view(np.uint32),
+                          O.duration_key(big.astype(np.uint64)))
+    # without encoding, a raw 4.0 s reads as a key: the f32 bits of a far longer duration
+    raw4 = torch.tensor(np.array([4_000_000_000, 1000], np.uint32).view(np.int32)).cuda()
+    st = ops.segment_stats_strided(raw4, 1, 2, 0, 2).cpu()
+    assert np.float32(st.max[0].item()) > np.float32(1e15)
+    st = ops.segment_stats_strided(ops.encode_ns_u32_(raw4), 1, 2, 0, 2).cpu()
+    assert np.float32(st.max[0].item()) == np.float32(np.float32(4e9) / np.float32(1000))
+    # the largest key of a u64 duration: f32(2^64) / 1000
+    ok = torch.tensor(np.array([5000, 0xF0200000, 3000], np.uint32).view(np.int32)).cuda()
+    st = ops.segment_stats_strided(ok, 1, 3, 0, 3, mode=ops.STATS_FAST).cpu()
+    assert np.float32(st.max[0].item()) == np.float32(np.float32(2.0**64) / np.float32(1000))
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_ring_capacity_beyond_32768(exact):
+    """statsMaxLenPerKernel above 32,768 (the reference's ring takes any
+    capacity, CuptiProfiler.h:49-51; CircularBuffer.h:23-70).  70,000 pushes of one key into a
+    65,536 ring, 40,000 of another and 20 of a third: the oracle's statistics, every field bit
+    for bit (rings this long sort in device scratch in both modes)."""
+    rng = np.random.default_rng(65536)
+    p = cupti.KernelProfiler(statsMaxLenPerKernel=65536, exact=exact)
+    try:
+        p.initialize()
+        p.start()
+        pushed = {"long_blk_1_1_1_grid_1_1_1": rng.integers(1000, 3_000_000, size=70_000, dtype=np.uint32),
+                  "mid_blk_1_1_1_grid_1_1_1": rng.integers(1000, 30_000, size=40_000, dtype=np.uint32),
+                  "short_blk_1_1_1_grid_1_1_1": rng.integers(1000, 30_000, size=20, dtype=np.uint32)}
+        pushed["mid_blk_1_1_1_grid_1_1_1"][::7] = 12345  # ties
+        for i in range(0, 70_000, 10_000):  # interleaved pushes
+            for k, v in pushed.items():
+                p.push(k, v[i:i + 10_000])
+        st = p.get_stats()
+        for k, v in pushed.items():
+            r = _oracle_slot_stats(v, 65536)
+            s = st[k]
+            got = (s.num_calls, np.float32(s.min), np.float32(s.max), np.float32(s.median),
+                   np.float32(s.avg), np.float32(s.stddev))
+            assert [np.float32(x).view(np.uint32) if i else x for i, x in enumerate(got)] == \
+                [np.float32(x).view(np.uint32) if i else x for i, x in enumerate(r)], k
+        assert st["long_blk_1_1_1_grid_1_1_1"].num_calls == 65536
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("mode", [ops.STATS_EXACT, ops.STATS_FAST])
+def test_segments_beyond_32768_strided_and_ragged(mode):
+    """The statistics entry points take retained segments of any length: strided segments of
+    50,000 kept of 60,000, and ragged ones of 33,000 / 100,000 / 5 next to each other."""
+    rng = np.random.default_rng(7)
+    m = rng.integers(1000, 5_000_000, size=(3, 60_000), dtype=np.uint32)
+    d = torch.from_numpy(m.view(np.int32)).cuda()
+    st = ops.segment_stats_strided(d, 3, 60_000, 0, 60_000, cap=50_000, mode=mode).cpu()
+    for s in range(3):
+        r = _oracle_slot_stats(m[s], 50_000)
+        got = (int(st.num[s]),) + tuple(np.float32(getattr(st, f)[s].item()) for f in ("min", "max", "med", "avg", "std"))
+        assert got == r, s
+    lens = [33_000, 100_000, 5]
+    vals = [rng.integers(1000, 5_000_000, size=n, dtype=np.uint32) for n in lens]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    d = torch.from_numpy(np.concatenate(vals).view(np.int32)).cuda()
+    st = ops.segment_stats_ragged(d, torch.from_numpy(off).cuda(), None, max(lens), cap=0, mode=mode).cpu()
+    for s, v in enumerate(vals):
+        r = _oracle_slot_stats(v, len(v))
+        got = (int(st.num[s]),) + tuple(np.float32(getattr(st, f)[s].item()) for f in ("min", "max", "med", "avg", "std"))
+        assert got == r, s

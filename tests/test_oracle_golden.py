@@ -162,3 +162,26 @@ def test_ns_to_us_reciprocal_multiply_identity():
     ref = f / np.float32(1000.0)
     got = (f.astype(np.float64) * (1.0 / 1000.0)).astype(np.float32)
     assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
+
+
+def test_wide_duration_kat_bit_exact():
+    """u64 durations of 2^32 ns and more: the reference's own conversion
+    (end - start) / 1000.0f and computeStats over it (compute_stats_wide_kat.json, made from the
+    reference build), reproduced by the oracle's conversion, and by the duration keys: decoding a
+    key gives back exactly the f32(ns) the reference divides."""
+    kat = _load("compute_stats_wide_kat.json")
+    conv = kat["conversion"]
+    ns = np.array(conv["ns"], np.uint64)
+    assert [_bits(v) for v in O.ns_to_us(ns)] == conv["us_bits"]
+    assert [_bits(O.lib().oracle_ns_to_us(int(n))) for n in conv["ns"]] == conv["us_bits"]
+    assert [_bits(v) for v in O.key_to_us(O.duration_key(ns))] == conv["us_bits"]
+    assert len(kat["cases"]) >= 10
+    for c in kat["cases"]:
+        x = np.array(c["ns"], np.uint64)
+        st = O.compute_stats(O.ring_linearize(O.ns_to_us(x), c["cap"]))
+        got = [int(st.num_calls)] + [_bits(v) for v in (st.min, st.max, st.median, st.avg, st.stddev)]
+        assert got == c["expect"], c["name"]
+        # the key route the HIP kernels take: keys -> f32 us, same bits
+        kst = O.compute_stats(O.ring_linearize(O.key_to_us(O.duration_key(x)), c["cap"]))
+        kgot = [int(kst.num_calls)] + [_bits(v) for v in (kst.min, kst.max, kst.median, kst.avg, kst.stddev)]
+        assert kgot == c["expect"], c["name"]

@@ -1,4 +1,4 @@
-"""profiles/pmc_c2_segment_stats.json from tools/profile_round.sh's --pmc passes."""
+"""profiles/pmc_c2_segment_stats.json from tools/history/profile_round.sh (or gpu_r03_profile.sh)'s --pmc passes."""
 import csv
 import glob
 import json
