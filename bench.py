@@ -158,7 +158,10 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         keep = min(s_push, cap)
         return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed,
                     kern_ms=float(np.mean(ks)) if ks else None,
-                    samples=R * K_local * keep, nseg=R * K_local, keep=keep)
+                    samples=R * K_local * keep, nseg=R * K_local, keep=keep,
+                    launch="hip_graph: whole reports, two in flight")
+    # N GPUs: the statistics, the shard's score partials and the combine replay as HIP graphs;
+    # only the all_gather of the partials between them is an eager collective
     g = rep.graph(ns, s_push) if use_graph else None
     if g is not None:
         for _ in range(max(1, warmup)):
@@ -185,8 +188,27 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if time_kernel else None
     keep = min(s_push, cap)
+    launch = ("eager" if g is None else
+              "hip_graph: statistics | score partials | eager all_gather | combine" if rep.exchange else
+              "hip_graph: statistics | rest")
     return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed, kern_ms=kern_ms,
-                samples=R * K_local * keep, nseg=R * K_local, keep=keep)
+                samples=R * K_local * keep, nseg=R * K_local, keep=keep, launch=launch)
+
+
+def score_digest(res) -> dict:
+    """Order-independent digest of a report's scores (NaN-free sums, f64): a strong-scaled leg's
+    digest on N ranks equals the single-GPU one up to the f64 rounding of the shard combine."""
+    return dict(rel_sum=float(np.nansum(res.gpu_relative)), ind_sum=float(np.nansum(res.gpu_individual)),
+                stragglers_rel=[int(i) for i in np.nonzero(res.stragglers_relative)[0]])
+
+
+def gather_labels(label: str, world: int):
+    """Every rank's label (its launch mode), rank order."""
+    if world == 1:
+        return [label]
+    out = [None] * world
+    torch.distributed.all_gather_object(out, label)
+    return out
 
 
 def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
@@ -221,6 +243,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     tmax = allreduce(elapsed, torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
     nrec = allreduce(float(R * N), torch.distributed.ReduceOp.SUM if world > 1 else None, world, dev)
     out = dict(ranks=R, kernels=K, records_per_rank=int(counts.sum()), cap=cap,
+               launch_per_rank=gather_labels("eager", world), scores=score_digest(res),
                ms_per_report=tmax / steps * 1e3, records_per_s=nrec * steps / tmax,
                bucket_plus_stats_ms=stats_ms,
                hbm_frac_of_report=R * N * RECORD_BYTES / (tmax / steps) / HBM_PEAK,
@@ -371,6 +394,7 @@ def main():
     world_reported = (torch.distributed.get_world_size()
                       if torch.distributed.is_available() and torch.distributed.is_initialized() else 1)
     sec_steps = max(10, args.steps // 2)  # the configs[2] / configs[3] legs
+    launch_per_rank = gather_labels(r["launch"], world)
 
     # ---------------- secondary: report latency at 4096 ranks (strong) ---------------
     lat = None
@@ -386,6 +410,7 @@ def main():
         s4 = r4["res"]
         k4 = comm_max(r4["kern_ms"], world, dev)
         lat = dict(ranks=C3["R"], kernels=C3["K"], samples_per_kernel=C3["s_push"],
+                   launch_per_rank=gather_labels(r4["launch"], world), scores=score_digest(s4),
                    ms_per_report=t4 / n4 * 1e3, samples_per_s=tot4 * n4 / t4,
                    stats_kernel_ms=k4,
                    stats_kernel_hbm_frac=(4 * r4["samples"] + 24 * r4["nseg"]) / (k4 * 1e-3) / HBM_PEAK,
@@ -486,7 +511,7 @@ def main():
                        "world_size": world, "world_size_reported": world_reported,
                        "kernels_per_rank": shard_sizes(K_global, world),
                        "backend": backend or "none (1 GPU)",
-                       "stats_mode": "fast", "launch": "eager" if args.no_graph else ("hip_graph, two reports in flight" if world == 1 else "hip_graph")},
+                       "stats_mode": "fast", "launch": r["launch"], "launch_per_rank": launch_per_rank},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic,

@@ -327,6 +327,10 @@ int nvrx_capture_flush(void);
 typedef struct nvrx_capture_counters {
     int64_t callbacks, headers, dispatches, callback_ns, flushes, flush_ns, runtime_kernels,
         own_kernels;
+    /* where the flushes' time goes: summed over flushes, the time from a flush's start to the
+     * first buffer callback it delivered, the callbacks delivered during flushes, and the time
+     * from a flush's last callback to its return */
+    int64_t flush_first_cb_ns, flush_callbacks, flush_tail_ns;
 } nvrx_capture_counters;
 int nvrx_capture_stats(nvrx_capture_counters* out);
 

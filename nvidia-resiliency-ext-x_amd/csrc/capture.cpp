@@ -49,6 +49,16 @@ struct Capture {
     // cost accounting (nvrx_capture_stats): callbacks, headers, dispatch records handed to the
     // profiler, time inside our callback, flushes and time inside rocprofiler_flush_buffer
     std::atomic<uint64_t> n_cb{0}, n_rec{0}, n_pushed{0}, cb_ns{0}, n_flush{0}, flush_ns{0};
+    // where a report-time flush's time goes: steady-clock ns of the flush in progress (0: none),
+    // and per flush the time to the first buffer callback it caused, the callbacks it caused,
+    // and the time from the end of its last callback to rocprofiler_flush_buffer's return
+    std::atomic<int64_t> flush_t0{0}, last_cb_end{0};
+    std::atomic<uint64_t> flush_first_cb_ns{0}, flush_cbs{0}, flush_tail_ns{0};
+    // delivery: 0 = buffer (records batched by rocprofiler-sdk, a report flushes the buffer),
+    // 1 = callback (each completed dispatch handed over as its completion is processed),
+    // 2 = callback_counted (1 + enqueues counted, so a flush waits for exactly those)
+    int delivery = 0;
+    std::atomic<uint64_t> n_enqueued{0}, n_completed{0};
     std::atomic<uint64_t> n_runtime{0};  // runtime copy / fill dispatches left out (below)
     bool keep_runtime = false;           // NVRX_CAPTURE_RUNTIME_KERNELS=1 keeps them
     // the library's own report kernels (get_stats / get_records / reset / ingest) are marked
@@ -131,57 +141,115 @@ std::string composite_name(const nvrx::DispatchKey& k) {
     return std::string(buf.data());
 }
 
+// One completed dispatch -> the reference's record, or false when it is not the job's kernel
+// (a report kernel of ours, or a runtime blit).
+enum class Kind { job, own, runtime };
+Kind to_dispatch(const rocprofiler_kernel_dispatch_info_t& di, uint64_t start, uint64_t end,
+                 uint64_t external, nvrx::DispatchRec& d) {
+    if (external == SELF_MARK) return Kind::own;  // a report kernel of ours
+    if (!cap().keep_runtime && runtime_blit(di.kernel_id)) return Kind::runtime;
+    // block dims = workgroup size; grid_size is in work-items, CUPTI's gridX..Z count blocks,
+    // including a partial last block (a module / ext launch whose global size is not a multiple
+    // of the workgroup): ceil
+    const uint32_t bx = di.workgroup_size.x, by = di.workgroup_size.y, bz = di.workgroup_size.z;
+    auto blocks = [](uint32_t g, uint32_t b) -> uint32_t {
+        return b ? (uint32_t)(((uint64_t)g + b - 1) / b) : 0;
+    };
+    d.key = {di.kernel_id, bx, by, bz, blocks(di.grid_size.x, bx), blocks(di.grid_size.y, by),
+             blocks(di.grid_size.z, bz)};
+    d.ns = end > start ? end - start : 0;
+    return Kind::job;
+}
+
+// a delivery callback's bookkeeping: in-flight count first, then the target (capture_detach
+// clears the target and then waits for the count to drain, so a callback never touches a
+// destroyed handle), and the flush accounting
+struct CallbackScope {
+    Capture& c;
+    std::chrono::steady_clock::time_point t0;
+    CallbackScope() : c(cap()) {
+        c.inflight.fetch_add(1);
+        t0 = std::chrono::steady_clock::now();
+        if (const int64_t f0 = c.flush_t0.load()) {  // delivered by a flush in progress
+            if (c.flush_cbs.fetch_add(1) == 0 || c.last_cb_end.load() < f0)  // its first callback
+                c.flush_first_cb_ns.fetch_add((uint64_t)(t0.time_since_epoch().count() - f0));
+        }
+    }
+    ~CallbackScope() {
+        const auto t1 = std::chrono::steady_clock::now();
+        c.cb_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
+        c.last_cb_end.store(t1.time_since_epoch().count());
+        c.inflight.fetch_sub(1);
+    }
+};
+
+// buffer delivery (NVRX_CAPTURE_DELIVERY=buffer): batches of records from rocprofiler-sdk's
+// buffer, at its watermark or at a flush
 void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
                         rocprofiler_record_header_t** headers, size_t num_headers, void*,
                         uint64_t) {
-    Capture& c = cap();
-    // in-flight count first, then the target: capture_detach clears the target and then
-    // waits for the count to drain, so a callback never touches a destroyed handle
-    c.inflight.fetch_add(1);
-    const auto t0 = std::chrono::steady_clock::now();
+    CallbackScope scope;
+    Capture& c = scope.c;
     nvrx_profiler* p = c.target.load();
-    if (p) {
-        thread_local std::vector<nvrx::DispatchRec> batch;
-        batch.clear();
-        uint64_t runtime = 0, own = 0;
-        for (size_t i = 0; i < num_headers; ++i) {
-            const rocprofiler_record_header_t* h = headers[i];
-            if (h->category != ROCPROFILER_BUFFER_CATEGORY_TRACING ||
-                h->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
-                continue;
-            auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
-            const rocprofiler_kernel_dispatch_info_t& di = r->dispatch_info;
-            if (r->correlation_id.external.value == SELF_MARK) {  // a report kernel of ours
-                ++own;
-                continue;
-            }
-            if (!c.keep_runtime && runtime_blit(di.kernel_id)) {
-                ++runtime;
-                continue;
-            }
-            // block dims = workgroup size; grid_size is in work-items, CUPTI's gridX..Z count
-            // blocks, including a partial last block (a module / ext launch whose global size is
-            // not a multiple of the workgroup): ceil
-            const uint32_t bx = di.workgroup_size.x, by = di.workgroup_size.y, bz = di.workgroup_size.z;
-            auto blocks = [](uint32_t g, uint32_t b) -> uint32_t {
-                return b ? (uint32_t)(((uint64_t)g + b - 1) / b) : 0;
-            };
-            nvrx::DispatchRec d;
-            d.key = {di.kernel_id, bx, by, bz, blocks(di.grid_size.x, bx), blocks(di.grid_size.y, by),
-                     blocks(di.grid_size.z, bz)};
-            d.ns = r->end_timestamp > r->start_timestamp ? r->end_timestamp - r->start_timestamp : 0;
-            batch.push_back(d);
+    if (!p) return;
+    thread_local std::vector<nvrx::DispatchRec> batch;
+    batch.clear();
+    uint64_t runtime = 0, own = 0;
+    for (size_t i = 0; i < num_headers; ++i) {
+        const rocprofiler_record_header_t* h = headers[i];
+        if (h->category != ROCPROFILER_BUFFER_CATEGORY_TRACING ||
+            h->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
+            continue;
+        auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
+        nvrx::DispatchRec d;
+        switch (to_dispatch(r->dispatch_info, r->start_timestamp, r->end_timestamp,
+                            r->correlation_id.external.value, d)) {
+            case Kind::own: ++own; break;
+            case Kind::runtime: ++runtime; break;
+            case Kind::job: batch.push_back(d); break;
         }
-        c.n_cb.fetch_add(1);
-        c.n_rec.fetch_add(num_headers);
-        c.n_pushed.fetch_add(batch.size());
-        c.n_runtime.fetch_add(runtime);
-        c.n_own.fetch_add(own);
-        if (!batch.empty()) nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
     }
-    c.cb_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                          std::chrono::steady_clock::now() - t0).count());
-    c.inflight.fetch_sub(1);
+    c.n_cb.fetch_add(1);
+    c.n_rec.fetch_add(num_headers);
+    c.n_pushed.fetch_add(batch.size());
+    c.n_runtime.fetch_add(runtime);
+    c.n_own.fetch_add(own);
+    if (!batch.empty()) nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
+}
+
+// callback delivery (NVRX_CAPTURE_DELIVERY=callback): rocprofiler-sdk's KERNEL_DISPATCH callback
+// tracing hands over each dispatch once the runtime has processed its completion signal -- no
+// buffer, so a report has nothing to flush but the completions still being processed.  With the
+// ENQUEUE operation too (=callback_counted) the enqueued dispatches are counted, and a flush
+// waits for exactly those completions.
+void dispatch_callback_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_user_data_t*, void*) {
+    Capture& c = cap();
+    if (record.kind != ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH) return;
+    if (record.operation == ROCPROFILER_KERNEL_DISPATCH_ENQUEUE) {
+        if (record.phase == ROCPROFILER_CALLBACK_PHASE_EXIT) c.n_enqueued.fetch_add(1);
+        return;
+    }
+    if (record.operation != ROCPROFILER_KERNEL_DISPATCH_COMPLETE) return;
+    {
+        CallbackScope scope;
+        nvrx_profiler* p = scope.c.target.load();
+        if (p) {
+            auto* r = static_cast<const rocprofiler_callback_tracing_kernel_dispatch_data_t*>(record.payload);
+            nvrx::DispatchRec d;
+            switch (to_dispatch(r->dispatch_info, r->start_timestamp, r->end_timestamp,
+                                record.correlation_id.external.value, d)) {
+                case Kind::own: c.n_own.fetch_add(1); break;
+                case Kind::runtime: c.n_runtime.fetch_add(1); break;
+                case Kind::job:
+                    c.n_pushed.fetch_add(1);
+                    nvrx::profiler_push_dispatches(p, &d, 1, composite_name);
+                    break;
+            }
+            c.n_cb.fetch_add(1);
+            c.n_rec.fetch_add(1);
+        }
+    }
+    c.n_completed.fetch_add(1, std::memory_order_release);  // after the record is pushed
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
@@ -200,23 +268,38 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
         c.self_marking = rocprofiler_configure_external_correlation_id_request_service(
                              c.disp_ctx, kinds, 1, external_corr_request, nullptr) == ROCPROFILER_STATUS_SUCCESS;
     }
-    size_t watermark = 1u << 20;  // ~ the Detector's CUPTI bufferSize (1 MB, cupti.py:25)
-    // NVRX_CAPTURE_WATERMARK overrides it, not below 64 KiB: with watermarks of a few KB
-    // rocprofiler-sdk (ROCm 7.2) was measured to lose dispatch records (tools/diag_capture.py)
-    if (const char* w = std::getenv("NVRX_CAPTURE_WATERMARK"))
-        watermark = std::max<size_t>(std::strtoull(w, nullptr, 10), (size_t)64 << 10);
-    if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, watermark, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
-                                  dispatch_buffer_cb, nullptr, &c.buffer) != ROCPROFILER_STATUS_SUCCESS)
-        return -1;
-    // a delivery thread of our own instead of rocprofiler-sdk's shared default: the report-time
-    // flush drops from 5.0-5.5 to 3.5-4.4 ms (profiles/r03/capture_cost.json, capture_cbthread_ab.log)
-    rocprofiler_callback_thread_t th{};
-    if (rocprofiler_create_callback_thread(&th) == ROCPROFILER_STATUS_SUCCESS)
-        (void)rocprofiler_assign_callback_thread(c.buffer, th);
-    if (rocprofiler_configure_buffer_tracing_service(c.disp_ctx,
-                                                     ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH,
-                                                     nullptr, 0, c.buffer) != ROCPROFILER_STATUS_SUCCESS)
-        return -1;
+    if (const char* m = std::getenv("NVRX_CAPTURE_DELIVERY")) {
+        const std::string v(m);
+        c.delivery = v == "callback" ? 1 : v == "callback_counted" ? 2 : 0;
+    }
+    if (c.delivery != 0) {
+        const rocprofiler_tracing_operation_t complete_only[] = {ROCPROFILER_KERNEL_DISPATCH_COMPLETE};
+        const rocprofiler_tracing_operation_t both[] = {ROCPROFILER_KERNEL_DISPATCH_ENQUEUE,
+                                                        ROCPROFILER_KERNEL_DISPATCH_COMPLETE};
+        if (rocprofiler_configure_callback_tracing_service(
+                c.disp_ctx, ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH,
+                c.delivery == 1 ? complete_only : both, c.delivery == 1 ? 1 : 2, dispatch_callback_cb,
+                nullptr) != ROCPROFILER_STATUS_SUCCESS)
+            return -1;
+    } else {
+        size_t watermark = 1u << 20;  // ~ the Detector's CUPTI bufferSize (1 MB, cupti.py:25)
+        // NVRX_CAPTURE_WATERMARK overrides it, not below 64 KiB: with watermarks of a few KB
+        // rocprofiler-sdk (ROCm 7.2) was measured to lose dispatch records (tools/diag_capture.py)
+        if (const char* w = std::getenv("NVRX_CAPTURE_WATERMARK"))
+            watermark = std::max<size_t>(std::strtoull(w, nullptr, 10), (size_t)64 << 10);
+        if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, watermark, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
+                                      dispatch_buffer_cb, nullptr, &c.buffer) != ROCPROFILER_STATUS_SUCCESS)
+            return -1;
+        // a delivery thread of our own instead of rocprofiler-sdk's shared default: the report-time
+        // flush drops from 5.0-5.5 to 3.5-4.4 ms (profiles/r03/capture_cost.json, capture_cbthread_ab.log)
+        rocprofiler_callback_thread_t th{};
+        if (rocprofiler_create_callback_thread(&th) == ROCPROFILER_STATUS_SUCCESS)
+            (void)rocprofiler_assign_callback_thread(c.buffer, th);
+        if (rocprofiler_configure_buffer_tracing_service(c.disp_ctx,
+                                                         ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH,
+                                                         nullptr, 0, c.buffer) != ROCPROFILER_STATUS_SUCCESS)
+            return -1;
+    }
     if (rocprofiler_start_context(c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
     c.ready = true;
     return 0;
@@ -225,7 +308,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
 void tool_fini(void*) {
     Capture& c = cap();
     if (!c.ready) return;
-    (void)rocprofiler_flush_buffer(c.buffer);
+    if (c.delivery == 0) (void)rocprofiler_flush_buffer(c.buffer);
     c.ready = false;
 }
 
@@ -260,14 +343,45 @@ int capture_stop(nvrx_profiler* p) {
     return rocprofiler_stop_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
 }
 
+// callback delivery: completions of dispatches that have finished on the device are processed by
+// the runtime's signal handler shortly after; wait for them -- for the counted enqueues exactly
+// (bounded: a kernel still running is delivered to a later report, as a CUPTI flush(0) leaves
+// it), else until no completion arrived for a quiet period
+bool wait_completions(Capture& c) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    if (c.delivery == 2) {
+        const uint64_t want = c.n_enqueued.load();
+        while (c.n_completed.load(std::memory_order_acquire) < want) {
+            if (clk::now() - t0 > std::chrono::milliseconds(20)) return true;
+            std::this_thread::yield();
+        }
+        return true;
+    }
+    uint64_t seen = c.n_completed.load(std::memory_order_acquire);
+    auto quiet = clk::now();
+    while (clk::now() - quiet < std::chrono::microseconds(200)) {
+        if (clk::now() - t0 > std::chrono::milliseconds(20)) break;
+        const uint64_t now = c.n_completed.load(std::memory_order_acquire);
+        if (now != seen) seen = now, quiet = clk::now();
+        std::this_thread::yield();
+    }
+    return true;
+}
+
 int capture_flush() {
     Capture& c = cap();
     if (!c.ready) return 0;
     const auto t0 = std::chrono::steady_clock::now();
-    const bool ok = rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS;
+    c.flush_t0.store(t0.time_since_epoch().count());
+    const bool ok = c.delivery == 0 ? rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS
+                                    : wait_completions(c);
+    const auto t1 = std::chrono::steady_clock::now();
+    const int64_t last = c.last_cb_end.load();
+    if (last >= c.flush_t0.load()) c.flush_tail_ns.fetch_add((uint64_t)(t1.time_since_epoch().count() - last));
+    c.flush_t0.store(0);
     c.n_flush.fetch_add(1);
-    c.flush_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                             std::chrono::steady_clock::now() - t0).count());
+    c.flush_ns.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
     return ok ? 0 : -1;
 }
 
@@ -285,7 +399,7 @@ void capture_self_end() { cap().self_tid.store(0, std::memory_order_release); }
 void capture_detach(nvrx_profiler* p) {
     Capture& c = cap();
     if (c.target.load() != p) return;
-    if (c.ready) (void)rocprofiler_flush_buffer(c.buffer);  // deliver what is pending, to p
+    if (c.ready) (void)capture_flush();  // deliver what is pending, to p
     nvrx_profiler* cur = p;
     if (c.target.compare_exchange_strong(cur, nullptr) && c.ready)
         (void)rocprofiler_stop_context(c.disp_ctx);
@@ -326,6 +440,9 @@ int nvrx_capture_stats(nvrx_capture_counters* out) {
     out->flush_ns = (int64_t)c.flush_ns.load();
     out->runtime_kernels = (int64_t)c.n_runtime.load();
     out->own_kernels = (int64_t)c.n_own.load();
+    out->flush_first_cb_ns = (int64_t)c.flush_first_cb_ns.load();
+    out->flush_callbacks = (int64_t)c.flush_cbs.load();
+    out->flush_tail_ns = (int64_t)c.flush_tail_ns.load();
     return NVRX_OK;
 }
 

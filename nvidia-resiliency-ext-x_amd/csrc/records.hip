@@ -23,6 +23,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "segment_kernels.h"
 
@@ -115,7 +116,8 @@ void records_bucket_kernel(
     const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
     int32_t* counts, int64_t stash_pairs, int64_t stage_cap, uint32_t cold_max,
-    nvrx_stats_soa tiny, uint32_t slot_lo, int64_t seg_stride, int pass) {
+    nvrx_stats_soa tiny, uint32_t slot_lo, int64_t seg_stride, int pass, int64_t t0,
+    int64_t nstreams_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
@@ -128,7 +130,7 @@ void records_bucket_kernel(
     u32x4* stash = (u32x4*)(stage + stage_cap);
     __shared__ uint32_t any_ovf;
     __shared__ uint32_t wtot[3][RB_WAVES];
-    const int64_t t = blockIdx.x;
+    const int64_t t = t0 + blockIdx.x;  // this launch's streams: [t0, t0 + gridDim.x)
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     const int64_t r0 = rec_off[t], r1 = rec_off[t + 1];
@@ -138,7 +140,7 @@ void records_bucket_kernel(
     // a slot table larger than one pass's LDS counters: pass p's buckets follow the regions of
     // passes 0..p-1, each as large as records_bucket_capacity's per-pass term
     const int64_t ns_off = pass == 0 ? 0 :
-        (int64_t)pass * (((rec_off[gridDim.x] + 3) & ~(int64_t)3) + (int64_t)gridDim.x * stream_slack(RB_PASS_SLOTS));
+        (int64_t)pass * (((rec_off[nstreams_total] + 3) & ~(int64_t)3) + nstreams_total * stream_slack(RB_PASS_SLOTS));
     const bool pairs = (((uintptr_t)rs) & 15) == 0;
     // The head of the stream -- up to RB_REGS x 64 x RB_WAVES record pairs -- is held in
     // registers between the passes, the waves sweeping it together (pair (u RB_WAVES + w) 64 +
@@ -407,28 +409,42 @@ int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
 }
 
 // dynamic LDS of a bucketing launch: a single workgroup may take the whole 160 KiB of a CU
-// (MI355X_MICROARCH.md), less the kernel's few static bytes
-constexpr size_t RB_LAUNCH_LDS = 160 * 1024 - 256;
+// (MI355X_MICROARCH.md), less the kernel's few static bytes.  NVRX_RB_LDS_KB (a build-time
+// tuning constant) caps it lower, so that class-kernel blocks fit beside a bucketing block
+// (records_stats' pipelined chunks, below).
+#ifndef NVRX_RB_LDS_KB
+#define NVRX_RB_LDS_KB 160
+#endif
+constexpr size_t RB_LAUNCH_LDS = (size_t)NVRX_RB_LDS_KB * 1024 - 256;
 // register-held record pairs per block, whatever the wave count: 16,384 pairs = 256 KiB =
 // 64 KiB per SIMD (half its register file) -- 4 waves x 64 pairs per lane (256 VGPRs),
 // 8 x 32 or 16 x 16 (64 VGPRs)
-constexpr int RB_REGS_PER_BLOCK = 16384;
-constexpr int RB_STAGE_KB = 96;  // LDS staging of the cold buckets
+#ifndef NVRX_RB_REGS_PER_BLOCK
+#define NVRX_RB_REGS_PER_BLOCK 16384
+#endif
+constexpr int RB_REGS_PER_BLOCK = NVRX_RB_REGS_PER_BLOCK;
+#ifndef NVRX_RB_STAGE_KB
+#define NVRX_RB_STAGE_KB 96
+#endif
+constexpr int RB_STAGE_KB = NVRX_RB_STAGE_KB;  // LDS staging of the cold buckets
 constexpr int RB_COLD = 512;     // largest cold bucket (records)
 
-// The one shipped configuration: 16 waves x 16 register pairs per lane (4 waves / SIMD, 128
+// The shipped configuration: 16 waves x 16 register pairs per lane (4 waves / SIMD, 128
 // VGPRs), LDS stash interleaved with pass 2, 96 KiB of cold-bucket staging, cold = keep <= 512.
 // The alternatives measured on configs[3] (4 / 8 waves, no register pairs, 2-3 blocks per CU,
 // other stage sizes and cold limits, no stash) are in DESIGN.md section 3.4.
-constexpr int RB_WAVES = 16;
+#ifndef NVRX_RB_WAVES
+#define NVRX_RB_WAVES 16
+#endif
+constexpr int RB_WAVES = NVRX_RB_WAVES;
 constexpr int RB_REGS = RB_REGS_PER_BLOCK / (64 * RB_WAVES);
 
-static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
-                                      int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
-                                      int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
-                                      const nvrx_stats_soa* tiny, uint32_t slot_lo, int64_t seg_stride,
-                                      int pass) {
-    if (nstreams <= 0 || nslots <= 0) return hipSuccess;
+static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* rec_off, int64_t t0,
+                                      int64_t nlaunch, int64_t nstreams, int64_t nslots, int64_t cap,
+                                      int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
+                                      int32_t* counts, hipStream_t st, const nvrx_stats_soa* tiny,
+                                      uint32_t slot_lo, int64_t seg_stride, int pass) {
+    if (nlaunch <= 0 || nslots <= 0) return hipSuccess;
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
     const nvrx_stats_soa tiny_soa = tiny ? *tiny : nvrx_stats_soa{};
@@ -450,36 +466,77 @@ static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* re
     int64_t stash_pairs = 0;
     if (lds_launch > fixed) stash_pairs = (int64_t)((lds_launch - fixed) / (16 * (size_t)RB_WAVES)) & ~(int64_t)63;
     if (fixed + (size_t)RB_WAVES * 16 * (size_t)stash_pairs > lds_launch) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
+    static size_t attr_lds = 0;
+    if (attr_lds < lds_launch) {
         const void* k = (const void*)records_bucket_kernel<RB_WAVES, RB_REGS>;
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, k);
         if (e != hipSuccess) return e;
-        if (fa.sharedSizeBytes + RB_LAUNCH_LDS > 160 * 1024) return hipErrorInvalidConfiguration;  // static LDS grew
-        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)RB_LAUNCH_LDS);
+        if (fa.sharedSizeBytes + lds_launch > 160 * 1024) return hipErrorInvalidConfiguration;  // static LDS grew
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_launch);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_lds = lds_launch;
     }
-    hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)nstreams), dim3(64 * RB_WAVES),
+    hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)nlaunch), dim3(64 * RB_WAVES),
                        lds_launch, st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns,
-                       counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa, slot_lo, seg_stride, pass);
+                       counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa, slot_lo, seg_stride, pass,
+                       t0, nstreams);
     return hipGetLastError();
+}
+
+// streams [t0, t0 + nlaunch) of nstreams
+static hipError_t records_bucket_range(const nvrx_record* recs, const int64_t* rec_off, int64_t t0,
+                                       int64_t nlaunch, int64_t nstreams, int64_t nslots, int64_t cap,
+                                       int force_stable, int64_t* seg_off, int32_t* seg_len,
+                                       uint32_t* out_ns, int32_t* counts, hipStream_t st,
+                                       const nvrx_stats_soa* tiny) {
+    // seg_off / seg_len / counts stay [nstreams][nslots]; pass p writes its slot range's columns
+    // and its buckets into out_ns after the regions of the passes before it
+    int pass = 0;
+    for (int64_t lo = 0; lo < nslots; lo += RB_PASS_SLOTS, ++pass) {
+        const int64_t m = std::min<int64_t>(RB_PASS_SLOTS, nslots - lo);
+        hipError_t e = records_bucket_pass(recs, rec_off, t0, nlaunch, nstreams, m, cap, force_stable,
+                                           seg_off, seg_len, out_ns, counts, st, tiny, (uint32_t)lo,
+                                           nslots, pass);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                           int64_t nslots, int64_t cap, int force_stable, int64_t* seg_off,
                           int32_t* seg_len, uint32_t* out_ns, int32_t* counts, hipStream_t st,
                           const nvrx_stats_soa* tiny) {
-    // seg_off / seg_len / counts stay [nstreams][nslots]; pass p writes its slot range's columns
-    // and its buckets into out_ns after the regions of the passes before it
-    int pass = 0;
-    for (int64_t lo = 0; lo < nslots; lo += RB_PASS_SLOTS, ++pass) {
-        const int64_t m = std::min<int64_t>(RB_PASS_SLOTS, nslots - lo);
-        hipError_t e = records_bucket_pass(recs, rec_off, nstreams, m, cap, force_stable, seg_off, seg_len,
-                                           out_ns, counts, st, tiny, (uint32_t)lo, nslots, pass);
+    return records_bucket_range(recs, rec_off, 0, nstreams, nstreams, nslots, cap, force_stable, seg_off,
+                                seg_len, out_ns, counts, st, tiny);
+}
+
+// Pipelined record statistics (NVRX_RS_CHUNKS > 1, a build-time constant): the streams are
+// bucketed in chunks on the caller's stream while the class kernels of the previous chunk run on
+// a second one, so that class-kernel blocks share the CUs with a bucketing block (which then
+// must leave them room: NVRX_RB_WAVES / NVRX_RB_LDS_KB).
+#ifndef NVRX_RS_CHUNKS
+#define NVRX_RS_CHUNKS 1
+#endif
+struct RsPipe {
+    hipStream_t side = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+static hipError_t rs_pipe(RsPipe*& out) {
+    static RsPipe* pipes[64] = {nullptr};
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (!pipes[dev]) {
+        RsPipe* p = new RsPipe{};
+        hipError_t e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&p->ev[i], hipEventDisableTiming);
         if (e != hipSuccess) return e;
+        pipes[dev] = p;
     }
+    out = pipes[dev];
     return hipSuccess;
 }
 
@@ -490,13 +547,41 @@ hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_
                          int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                          const nvrx_stats_soa& out, uint32_t* col_ref, hipStream_t st) {
-    hipError_t e = records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off, seg_len, out_ns,
-                                  counts, st, &out);
-    if (e != hipSuccess) return e;
     const int64_t keep = std::max<int64_t>(1, (cap > 0 && max_len > cap) ? cap : max_len);
-    e = segment_stats_ragged(out_ns, seg_off, seg_len, nstreams * nslots, keep, 0, mode, true, out,
-                             nullptr, 0, st);
-    if (e != hipSuccess || !col_ref) return e;
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    if (hipError_t e = hipStreamIsCapturing(st, &cst); e != hipSuccess) return e;
+    const int64_t chunks = std::min<int64_t>(NVRX_RS_CHUNKS, nstreams);
+    if (chunks <= 1 || cst != hipStreamCaptureStatusNone) {
+        hipError_t e = records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off, seg_len, out_ns,
+                                      counts, st, &out);
+        if (e != hipSuccess) return e;
+        e = segment_stats_ragged(out_ns, seg_off, seg_len, nstreams * nslots, keep, 0, mode, true, out,
+                                 nullptr, 0, st);
+        if (e != hipSuccess || !col_ref) return e;
+        return kernel_ref(out.num, out.med, nstreams, nslots, nullptr, col_ref, st);
+    }
+    RsPipe* pp = nullptr;
+    if (hipError_t e = rs_pipe(pp); e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    for (int64_t c = 0; c < chunks && e == hipSuccess; ++c) {
+        const int64_t t0 = nstreams * c / chunks, t1 = nstreams * (c + 1) / chunks;
+        e = records_bucket_range(recs, rec_off, t0, t1 - t0, nstreams, nslots, cap, 0, seg_off, seg_len,
+                                 out_ns, counts, st, &out);
+        if (e == hipSuccess) e = hipEventRecord(pp->ev[0], st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(pp->side, pp->ev[0], 0);
+        if (e != hipSuccess) break;
+        const int64_t g0 = t0 * nslots;
+        const nvrx_stats_soa o{out.num + g0, out.min + g0, out.max + g0, out.med + g0, out.avg + g0,
+                               out.std + g0};
+        e = segment_stats_ragged(out_ns, seg_off + g0, seg_len + g0, (t1 - t0) * nslots, keep, 0, mode,
+                                 true, o, nullptr, 0, pp->side);
+    }
+    // joined on every path
+    const hipError_t j1 = hipEventRecord(pp->ev[1], pp->side);
+    const hipError_t j2 = j1 == hipSuccess ? hipStreamWaitEvent(st, pp->ev[1], 0) : j1;
+    if (e != hipSuccess) return e;
+    if (j2 != hipSuccess) return j2;
+    if (!col_ref) return hipSuccess;
     return kernel_ref(out.num, out.med, nstreams, nslots, nullptr, col_ref, st);
 }
 

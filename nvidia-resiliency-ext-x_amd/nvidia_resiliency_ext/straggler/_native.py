@@ -59,7 +59,8 @@ class Record(ctypes.Structure):
 class CaptureCounters(ctypes.Structure):
     _fields_ = [("callbacks", i64), ("headers", i64), ("dispatches", i64),
                 ("callback_ns", i64), ("flushes", i64), ("flush_ns", i64), ("runtime_kernels", i64),
-                ("own_kernels", i64)]
+                ("own_kernels", i64), ("flush_first_cb_ns", i64), ("flush_callbacks", i64),
+                ("flush_tail_ns", i64)]
 
 
 class ProfilerConfig(ctypes.Structure):

@@ -194,12 +194,28 @@ class MatrixReporter:
                        finalize=self._outputs(b), done=done, reset_col_ref=reset)
             self._colref_clean = fused
             return
+        self._scores_partials()
+        self._exchange()
+        self._finalize()
+
+    # -- the N-GPU scoring in three phases: per-rank partials of this shard's kernels (HIP), the
+    # all_gather of the partials (RCCL / gloo), the combine in shard order (HIP) --
+    def _scores_partials(self) -> None:
+        R, K = self.R, self.K
+        st = self.stats.view(R, K)
+        ref = self.col_ref.view(torch.float32)[:K] if self.relative else None
+        missing = self.col_ref[K:2 * K] if self.relative else None
+        fused = self._fuse_ref()
         if not fused:
             self.err.zero_()
         ops.scores(st.num, st.med, st.avg, col_valid=self.col_valid, ref=ref,
                    ref_missing=missing, hist=self.hist, partials=self.partials, err=self.err,
-                   done=done, reset_col_ref=reset)
+                   done=self.done if fused else None,
+                   reset_col_ref=self.col_ref[:2 * K] if fused else None)
         self._colref_clean = fused
+
+    def _exchange(self) -> None:
+        R = self.R
         flat = self.gathered.view(self.world * R, 6)
         if self.gloo:  # gloo collectives take host tensors
             hg = torch.empty((self.world * R, 6), dtype=torch.float64)
@@ -207,6 +223,9 @@ class MatrixReporter:
             flat.copy_(hg)
         else:          # RCCL over xGMI, device to device
             torch.distributed.all_gather_into_tensor(flat, self.partials, group=self.group)
+
+    def _finalize(self) -> None:
+        R = self.R
         o = self._outputs()
         ops.finalize_scores(self.gathered, R, self.world, self.round_f32, self.thr_rel,
                             self.thr_ind, rel=self.relative, ind=self.individual, err=self.err,
@@ -262,7 +281,17 @@ class ReportGraph:
         with torch.cuda.graph(self.stats):
             rep.compute_stats(ns, s_push)
         self.rest = self.full = None
-        if not rep.exchange:
+        if rep.exchange:
+            # N GPUs: the shard's partials and the combine (+ the result copy) as graphs too;
+            # only the all_gather of the partials between them runs eagerly
+            self.partials = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.partials):
+                rep._scores_partials()
+            self.finalize = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.finalize):
+                rep._finalize()
+                rep.h_out.copy_(rep.out, non_blocking=True)
+        else:
             self.rest = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.rest):
                 rep.compute_scores()
@@ -278,9 +307,12 @@ class ReportGraph:
 
     def run_rest(self) -> BatchResult:
         rep = self.rep
-        if self.rest is None:
-            rep.compute_scores()
-            return rep.land()
+        if self.rest is None:  # N GPUs: partials graph, eager all_gather, combine graph
+            self.partials.replay()
+            rep._exchange()
+            self.finalize.replay()
+            _wait(rep.device)
+            return rep._unpack()
         self.rest.replay()
         _wait(rep.device)
         return rep._unpack()

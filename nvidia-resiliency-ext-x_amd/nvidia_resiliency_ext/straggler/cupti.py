@@ -184,20 +184,20 @@ class KernelProfiler:
         N.call("nvrx_profiler_generation", self._h, ctypes.byref(g))
         return int(g.value)
 
-    def ingest(self, records, stream=None, generation: Optional[int] = None) -> None:
+    def ingest(self, records, stream=None, *, generation: int) -> None:
         """Append DEVICE records: an int32/uint32 tensor [n, 2] of {slot, ns} (registered slots,
         push order) resident on the profiler's device, copied into the device record log on
-        `stream` (default: the current stream) -- no host round trip.  ``generation``: the
-        ``self.generation`` the slots were registered under (default: the current one); a
-        reset since then raises RuntimeError.  Records of unregistered slots are dropped."""
+        `stream` (default: the current stream) -- no host round trip.  ``generation`` (required):
+        the ``self.generation`` read after registering the slots; a reset since then raises
+        RuntimeError instead of filing the records under slots that now name other kernels.
+        Records of unregistered slots are dropped."""
         import torch
 
         N.require_device(records, "records")
         if records.dim() != 2 or records.shape[1] != 2 or records.element_size() != 4:
             raise ValueError("records must be a [n, 2] tensor of 32-bit {slot, ns}")
         records = records.contiguous()
-        gen = self.generation if generation is None else int(generation)
-        N.call("nvrx_profiler_ingest", self._h, records.data_ptr(), records.shape[0], gen,
+        N.call("nvrx_profiler_ingest", self._h, records.data_ptr(), records.shape[0], int(generation),
                N.stream_handle(stream if stream is not None else torch.cuda.current_stream(records.device)))
 
     def saturated(self) -> int:
@@ -342,7 +342,13 @@ class CuptiManager:
         with self.lock:
             return self.cupti_ext.register_kernel(name)
 
-    def ingest(self, records, stream=None, generation=None):
+    @property
+    def generation(self) -> int:
+        """Slot-numbering generation to pass to ingest() (read after register_kernel)."""
+        with self.lock:
+            return self.cupti_ext.generation
+
+    def ingest(self, records, stream=None, *, generation: int):
         """Device-resident {slot, ns} records from an external tracer into the active run."""
         with self.lock:
-            self.cupti_ext.ingest(records, stream, generation)
+            self.cupti_ext.ingest(records, stream, generation=generation)

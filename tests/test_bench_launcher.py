@@ -66,3 +66,14 @@ def test_launcher_four_ranks_gloo_rehearsal():
     lat, zipf = line["latency_4096_ranks"], line["zipf_16384_ranks"]
     assert lat["straggler_sets_exact"] is True and sum(lat["kernels_per_rank"]) == 2048
     assert zipf["straggler_sets_exact"] is True and sum(zipf["kernels_per_rank"]) == 2048
+    # every rank runs the same launch mode -- statistics, partials and the
+    # combine as graphs, only the all_gather eager -- and the strong-scaled legs report what one
+    # GPU reports (f64 combine order aside)
+    want = "hip_graph: statistics | score partials | eager all_gather | combine"
+    assert cfg["launch_per_rank"] == [want] * 4 and lat["launch_per_rank"] == [want] * 4
+    one = _run(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
+    for leg in ("latency_4096_ranks", "zipf_16384_ranks"):
+        a, b = line[leg]["scores"], one[leg]["scores"]
+        assert a["stragglers_rel"] == b["stragglers_rel"], leg
+        for f in ("rel_sum", "ind_sum"):
+            assert abs(a[f] - b[f]) <= 1e-9 * abs(b[f]), (leg, f, a[f], b[f])

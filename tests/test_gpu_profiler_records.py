@@ -257,14 +257,14 @@ def test_profiler_ingest_device_records():
         slots = [p.register_kernel(n) for n in names]
         dev = torch.from_numpy(np.stack([np.full(5, slots[0], np.uint32),
                                          np.arange(5, dtype=np.uint32) + 1], 1).view(np.int32)).cuda()
-        p.ingest(dev)  # stopped: ignored
+        p.ingest(dev, generation=p.generation)  # stopped: ignored
         p.start()
         host_ns = rng.integers(1000, 90_000, size=80, dtype=np.uint32)
         p.push(names[0], host_ns)
         ing = np.stack([rng.integers(0, 3, size=300).astype(np.uint32),
                         rng.integers(1000, 90_000, size=300, dtype=np.uint32)], 1)
         ing[7, 0] = 3  # not a registered slot: not counted
-        p.ingest(torch.from_numpy(np.ascontiguousarray(ing).view(np.int32)).cuda())
+        p.ingest(torch.from_numpy(np.ascontiguousarray(ing).view(np.int32)).cuda(), generation=p.generation)
         st = p.get_stats()
         for s, name in zip(slots, names):
             d = ing[(ing[:, 0] == s), 1]
@@ -298,7 +298,7 @@ def test_profiler_ingest_rejects_slots_from_before_a_reset():
         with pytest.raises(RuntimeError, match="generation"):
             p.ingest(rec(old, 7000), generation=g_old)
         p.ingest(rec(new, 3000), generation=p.generation)
-        p.ingest(rec(1, 5000))  # slot 1 is not registered yet: dropped
+        p.ingest(rec(1, 5000), generation=p.generation)  # slot 1 is not registered yet: dropped
         later = p.register_kernel("later_blk_1_1_1_grid_1_1_1")
         assert later == 1
         st = p.get_stats()

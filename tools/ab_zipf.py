@@ -32,7 +32,7 @@ for _ in range(n):
     e[1].record()
     torch.cuda.synchronize()
     ts += e[0].elapsed_time(e[1])
-if os.environ.get("AB_DUMP"):
+if os.environ.get("AB_DUMP"):  # the statistics of the first call (parity of A/B variants)
     torch.save({f: getattr(ref, f) for f in ("num", "min", "max", "med", "avg", "std")}, os.environ["AB_DUMP"])
 env = {k: v for k, v in os.environ.items() if k.startswith("NVRX_")}
 print(f"pkg={os.environ.get('AB_PKG', 'tree')} R={R} records={R*N} records_stats_ms={ts/n:.3f} "

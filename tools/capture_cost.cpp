@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -67,6 +68,8 @@ int main(int argc, char** argv) {
         stop_us = now_us() - s0;
     }
     nvrx_capture_stats(&c1);
+    nvrx_capture_counters cf0{}, cf1{};
+    nvrx_capture_stats(&cf0);
     // report-time flush latency against the records waiting (0, 100, 1000, 10000 dispatches)
     std::vector<double> flush_us;
     const int waits[] = {0, 100, 1000, 10000};
@@ -77,6 +80,8 @@ int main(int argc, char** argv) {
         nvrx_capture_flush();
         flush_us.push_back(now_us() - f0);
     }
+    nvrx_capture_stats(&cf1);
+    const double nf = (double)std::max<int64_t>(1, cf1.flushes - cf0.flushes);
     // the profiler's get_stats (flush + device bucketing + EXACT stats + download)
     double gs_us = 0, gs2_us = 0;
     int64_t kernels = 0;
@@ -97,11 +102,15 @@ int main(int argc, char** argv) {
            "\"records_delivered\": %lld, \"callback_us_per_record\": %.4f, "
            "\"flush_us\": {\"0\": %.1f, \"100\": %.1f, \"1000\": %.1f, \"10000\": %.1f}, "
            "\"get_stats_us_first\": %.1f, \"get_stats_us\": %.1f, \"stop_us\": %.1f, \"kernels\": %lld, "
-           "\"flushes\": %lld, \"flush_ms_total\": %.3f}\n",
+           "\"flushes\": %lld, \"flush_ms_total\": %.3f, \"delivery\": \"%s\", "
+           "\"flush_first_callback_us\": %.1f, \"flush_callbacks\": %.1f, \"flush_tail_us\": %.1f}\n",
            mode, avail, n, (t1 - t0) / n, (t2 - t0) / n, (long long)(c1.dispatches - c0.dispatches),
            c1.dispatches > c0.dispatches ? (c1.callback_ns - c0.callback_ns) * 1e-3 / (double)(c1.dispatches - c0.dispatches) : 0.0,
            flush_us[0], flush_us[1], flush_us[2], flush_us[3], gs_us, gs2_us, stop_us, (long long)kernels,
-           (long long)c2.flushes, c2.flush_ns * 1e-6);
+           (long long)c2.flushes, c2.flush_ns * 1e-6,
+           getenv("NVRX_CAPTURE_DELIVERY") ? getenv("NVRX_CAPTURE_DELIVERY") : "buffer",
+           (cf1.flush_first_cb_ns - cf0.flush_first_cb_ns) * 1e-3 / nf,
+           (cf1.flush_callbacks - cf0.flush_callbacks) / nf, (cf1.flush_tail_ns - cf0.flush_tail_ns) * 1e-3 / nf);
     if (p) nvrx_profiler_destroy(p);
     return 0;
 }
