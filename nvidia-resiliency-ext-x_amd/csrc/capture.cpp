@@ -54,10 +54,14 @@ struct Capture {
     // and the time from the end of its last callback to rocprofiler_flush_buffer's return
     std::atomic<int64_t> flush_t0{0}, last_cb_end{0};
     std::atomic<uint64_t> flush_first_cb_ns{0}, flush_cbs{0}, flush_tail_ns{0};
-    // delivery: 0 = buffer (records batched by rocprofiler-sdk, a report flushes the buffer),
-    // 1 = callback (each completed dispatch handed over as its completion is processed),
-    // 2 = callback_counted (1 + enqueues counted, so a flush waits for exactly those)
-    int delivery = 0;
+    // delivery (NVRX_CAPTURE_DELIVERY): 0 = buffer (records batched by rocprofiler-sdk, a report
+    // flushes the buffer: ~3.4-5 ms whenever records are pending, of which all but ~35 us come
+    // after our callback has returned -- rocprofiler-sdk's own wait), 1 = callback (each completed
+    // dispatch handed over as its completion is processed; a flush waits for a 200 us quiet
+    // period), 2 = callback_counted, the default (1 + the enqueues counted, so a flush waits for
+    // exactly those completions: ~1 us when the device is idle).  profiles/r04/capture_delivery.json
+    // has the per-dispatch and flush costs of the three, interleaved on one box.
+    int delivery = 2;
     std::atomic<uint64_t> n_enqueued{0}, n_completed{0};
     std::atomic<uint64_t> n_runtime{0};  // runtime copy / fill dispatches left out (below)
     bool keep_runtime = false;           // NVRX_CAPTURE_RUNTIME_KERNELS=1 keeps them
@@ -270,7 +274,7 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     }
     if (const char* m = std::getenv("NVRX_CAPTURE_DELIVERY")) {
         const std::string v(m);
-        c.delivery = v == "callback" ? 1 : v == "callback_counted" ? 2 : 0;
+        c.delivery = v == "buffer" ? 0 : v == "callback" ? 1 : 2;
     }
     if (c.delivery != 0) {
         const rocprofiler_tracing_operation_t complete_only[] = {ROCPROFILER_KERNEL_DISPATCH_COMPLETE};

@@ -206,9 +206,13 @@ mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
 assert hip.hipModuleLoad(ctypes.byref(mod), PROBE.encode()) == 0
 assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"nvrx_grid_probe") == 0
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-a_out, a_n = ctypes.c_void_p(buf.data_ptr()), ctypes.c_uint32(1000)
-params = (ctypes.c_void_p * 2)(ctypes.cast(ctypes.byref(a_out), ctypes.c_void_p),
-                               ctypes.cast(ctypes.byref(a_n), ctypes.c_void_p))
+class Args(ctypes.Structure):  # the kernel's argument buffer: (unsigned* out, unsigned n)
+    _fields_ = [("out", ctypes.c_void_p), ("n", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+args = Args(buf.data_ptr(), 1000, 0)
+size = ctypes.c_size_t(ctypes.sizeof(args))
+# the "extra" form (HIP_LAUNCH_PARAM_BUFFER_POINTER / _SIZE / _END), which the ext launch takes
+extra = (ctypes.c_void_p * 5)(1, ctypes.cast(ctypes.byref(args), ctypes.c_void_p), 2,
+                              ctypes.cast(ctypes.byref(size), ctypes.c_void_p), 3)
 hip.hipExtModuleLaunchKernel.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [
     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
     ctypes.c_void_p, ctypes.c_uint32]
@@ -219,7 +223,7 @@ def section():
     assert rc == 0, ("hipMemsetAsync", rc)
     ops.stragglers(score, 0.5, out=m)  # the one real kernel: 256 threads, 4 blocks
     # global size 1000 over workgroups of 256: a partial last block, 4 blocks as CUPTI counts
-    rc = hip.hipExtModuleLaunchKernel(fn, 1000, 1, 1, 256, 1, 1, 0, stream, params, None,
+    rc = hip.hipExtModuleLaunchKernel(fn, 1000, 1, 1, 256, 1, 1, 0, stream, None, extra,
                                       None, None, 0)
     assert rc == 0, ("hipExtModuleLaunchKernel", rc)
 section()  # warm-up, stopped: nothing recorded

@@ -17,7 +17,8 @@ def test_pipelined_matches_sequential_reports():
     b = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
     ns = torch.empty_like(seqs[0])
     pipe = b.pipelined(ns, S, timing=True)
-    b.reset_history()  # the capture's eager pass ran one report
+    # (no reset_history: the warm-up pass of the capture leaves the individual history as it
+    # was, ADVICE r03 -- ns holds uninitialised memory here)
     want, got = [], []
     ns.copy_(seqs[0])
     for i in range(5):
@@ -57,3 +58,38 @@ def test_pipelined_two_in_flight():
     assert outs[0][1] is None and outs[1][1] is not None
     for res, _ in outs + [pipe.collect()]:
         np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
+
+
+@pytest.mark.parametrize("R", [8, 300])
+def test_error_flags_per_report_and_column_reference_reset(R):
+    """The scores epilogue (nvrx_score_args.done, R <= 256) stores each report's error bits and
+    re-initialises the column reference itself: a report whose MED is 0 (ZeroDivisionError in
+    the reference) sets err bit 1, the next clean report reads 0 again, and its reference (hence
+    its relative scores) is that of its own input alone -- eager, graph-replayed and pipelined.
+    R = 300 takes the column-reduction path (no epilogue; err zeroed per report)."""
+    K, S = 64, 200
+    good = synth.synth_matrix(R, K, S, seed=7, device="cuda")
+    bad = good.clone()
+    bad[1, 3, :] = 0  # kernel 3 of rank 1: every retained duration 0 ns -> MED 0
+    fast = good.clone().view(R, K, S)
+    fast[:, :, :] //= 2  # halved durations: a different per-kernel reference
+    fresh = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
+    want_fast = fresh.report(fast, S)
+    rep = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
+    assert rep.report(bad, S).err & 1
+    assert rep.report(good, S).err == 0
+    rep.reset_history()
+    np.testing.assert_array_equal(rep.report(fast, S).gpu_relative, want_fast.gpu_relative)
+    g = rep.graph(good, S)
+    good_copy = good.clone()
+    assert g.run().err == 0
+    good.copy_(bad)
+    assert g.run().err & 1
+    good.copy_(good_copy)
+    assert g.run().err == 0
+    pipe = rep.pipelined(good, S)
+    for src, want in ((bad, 1), (good_copy, 0), (bad, 1)):
+        good.copy_(src)
+        pipe.submit()
+        res, _ = pipe.collect()
+        assert (res.err & 1) == want
