@@ -620,6 +620,7 @@ int nvrx_profiler_stop(nvrx_profiler* p) {
     NVRX_CHECK_ARG(p, "nvrx_profiler_stop: null handle");
     std::lock_guard<std::mutex> ctx(p->ctx_mu);  // not inside a report's pause
     const int rc = nvrx::capture_stop(p);
+    nvrx::capture_drain(p);  // callback delivery: completed dispatches queued so far (before p->mu)
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->started) std::fprintf(stderr, "CuptiProfiler::stopProfiling called while not profiling.\n");
     p->started = false;

@@ -56,13 +56,22 @@ struct Capture {
     std::atomic<uint64_t> flush_first_cb_ns{0}, flush_cbs{0}, flush_tail_ns{0};
     // delivery (NVRX_CAPTURE_DELIVERY): 0 = buffer (records batched by rocprofiler-sdk, a report
     // flushes the buffer: ~3.4-5 ms whenever records are pending, of which all but ~35 us come
-    // after our callback has returned -- rocprofiler-sdk's own wait), 1 = callback (each completed
-    // dispatch handed over as its completion is processed; a flush waits for a 200 us quiet
-    // period), 2 = callback_counted, the default (1 + the enqueues counted, so a flush waits for
-    // exactly those completions: ~1 us when the device is idle).  profiles/r04/capture_delivery.json
-    // has the per-dispatch and flush costs of the three, interleaved on one box.
-    int delivery = 2;
+    // after our callback has returned -- rocprofiler-sdk's own wait), 1 = callback, the default
+    // (each completed dispatch handed over as its completion is processed; a flush waits for a
+    // 200 us quiet period), 2 = callback_counted (1 + the enqueues counted, so a flush waits for
+    // exactly those completions, ~1 us -- but the enqueue callbacks on the launching thread cost
+    // the training step more).  GPT-2 small, batch 8, profiling_interval 1, interleaved:
+    // step overhead 9.2 / 11.2 / 13.7 % (callback / buffer / counted, medians of 3), report-time
+    // flush 0.2 / 3.5 / 0.005 ms (profiles/r04/live_delivery.json, capture_delivery.json).
+    int delivery = 1;
     std::atomic<uint64_t> n_enqueued{0}, n_completed{0};
+    // callback delivery runs on the runtime's completion (signal-handler) thread, which must never
+    // wait for the profiler's lock: the caller's thread may hold it across a HIP call that needs
+    // that very thread (a deadlock, seen at stop()'s drain).  Completed dispatches are therefore
+    // queued under a lock held only for the append, and moved into the profiler by the caller's
+    // thread (capture_drain: at every flush and stop).
+    std::mutex qmu;
+    std::vector<nvrx::DispatchRec> queue;
     std::atomic<uint64_t> n_runtime{0};  // runtime copy / fill dispatches left out (below)
     bool keep_runtime = false;           // NVRX_CAPTURE_RUNTIME_KERNELS=1 keeps them
     // the library's own report kernels (get_stats / get_records / reset / ingest) are marked
@@ -236,18 +245,18 @@ void dispatch_callback_cb(rocprofiler_callback_tracing_record_t record, rocprofi
     if (record.operation != ROCPROFILER_KERNEL_DISPATCH_COMPLETE) return;
     {
         CallbackScope scope;
-        nvrx_profiler* p = scope.c.target.load();
-        if (p) {
+        if (scope.c.target.load()) {  // queued for the attached profiler (capture_drain)
             auto* r = static_cast<const rocprofiler_callback_tracing_kernel_dispatch_data_t*>(record.payload);
             nvrx::DispatchRec d;
             switch (to_dispatch(r->dispatch_info, r->start_timestamp, r->end_timestamp,
                                 record.correlation_id.external.value, d)) {
                 case Kind::own: c.n_own.fetch_add(1); break;
                 case Kind::runtime: c.n_runtime.fetch_add(1); break;
-                case Kind::job:
-                    c.n_pushed.fetch_add(1);
-                    nvrx::profiler_push_dispatches(p, &d, 1, composite_name);
+                case Kind::job: {
+                    std::lock_guard<std::mutex> lk(c.qmu);
+                    c.queue.push_back(d);
                     break;
+                }
             }
             c.n_cb.fetch_add(1);
             c.n_rec.fetch_add(1);
@@ -373,9 +382,26 @@ bool wait_completions(Capture& c) {
     return true;
 }
 
+void capture_drain(nvrx_profiler* p) {
+    Capture& c = cap();
+    if (c.delivery == 0 || !p) return;
+    thread_local std::vector<nvrx::DispatchRec> batch;
+    batch.clear();
+    {
+        std::lock_guard<std::mutex> lk(c.qmu);
+        batch.swap(c.queue);
+    }
+    if (batch.empty()) return;
+    c.n_pushed.fetch_add(batch.size());
+    nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
+}
+
 int capture_flush() {
     Capture& c = cap();
     if (!c.ready) return 0;
+    struct Drain {  // whatever completed is moved into the attached profiler, on this thread
+        ~Drain() { capture_drain(cap().target.load()); }
+    } drain;
     const auto t0 = std::chrono::steady_clock::now();
     c.flush_t0.store(t0.time_since_epoch().count());
     const bool ok = c.delivery == 0 ? rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS
@@ -408,6 +434,7 @@ void capture_detach(nvrx_profiler* p) {
     if (c.target.compare_exchange_strong(cur, nullptr) && c.ready)
         (void)rocprofiler_stop_context(c.disp_ctx);
     while (c.inflight.load() != 0) std::this_thread::yield();  // callbacks that loaded p
+    capture_drain(p);  // what those callbacks queued is p's, not the next profiler's
 }
 
 }  // namespace nvrx

@@ -87,6 +87,8 @@ bool capture_ready();
 int capture_start(nvrx_profiler* p);
 int capture_stop(nvrx_profiler* p);
 int capture_flush();
+// callback delivery: move the completed dispatches queued so far into p (the caller's thread)
+void capture_drain(nvrx_profiler* p);
 void capture_detach(nvrx_profiler* p);
 // mark the calling thread's kernel dispatches as the library's own (not captured) until
 // capture_self_end; false when the capture is off or rocprofiler-sdk cannot mark them

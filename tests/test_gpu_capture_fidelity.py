@@ -206,13 +206,9 @@ mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
 assert hip.hipModuleLoad(ctypes.byref(mod), PROBE.encode()) == 0
 assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"nvrx_grid_probe") == 0
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-class Args(ctypes.Structure):  # the kernel's argument buffer: (unsigned* out, unsigned n)
-    _fields_ = [("out", ctypes.c_void_p), ("n", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
-args = Args(buf.data_ptr(), 1000, 0)
-size = ctypes.c_size_t(ctypes.sizeof(args))
-# the "extra" form (HIP_LAUNCH_PARAM_BUFFER_POINTER / _SIZE / _END), which the ext launch takes
-extra = (ctypes.c_void_p * 5)(1, ctypes.cast(ctypes.byref(args), ctypes.c_void_p), 2,
-                              ctypes.cast(ctypes.byref(size), ctypes.c_void_p), 3)
+a_out, a_n = ctypes.c_void_p(buf.data_ptr()), ctypes.c_uint32(1000)
+params = (ctypes.c_void_p * 2)(ctypes.cast(ctypes.byref(a_out), ctypes.c_void_p),
+                               ctypes.cast(ctypes.byref(a_n), ctypes.c_void_p))
 hip.hipExtModuleLaunchKernel.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [
     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
     ctypes.c_void_p, ctypes.c_uint32]
@@ -222,10 +218,14 @@ def section():
     rc = hip.hipMemsetAsync(ctypes.c_void_p(dst.data_ptr()), 0, dst.numel() * 4, stream)
     assert rc == 0, ("hipMemsetAsync", rc)
     ops.stragglers(score, 0.5, out=m)  # the one real kernel: 256 threads, 4 blocks
-    # global size 1000 over workgroups of 256: a partial last block, 4 blocks as CUPTI counts
-    rc = hip.hipExtModuleLaunchKernel(fn, 1000, 1, 1, 256, 1, 1, 0, stream, None, extra,
+    # a module kernel through the ext launch (global size in work-items): 1024 over workgroups
+    # of 256 = 4 blocks.  (HIP refuses a global size that is not a multiple of the workgroup,
+    # tools/probe_ext_launch.py, so a partial last block -- counted by the capture's ceil, as
+    # CUPTI's gridX counts it -- cannot be produced through HIP)
+    rc = hip.hipExtModuleLaunchKernel(fn, 1024, 1, 1, 256, 1, 1, 0, stream, params, None,
                                       None, None, 0)
-    assert rc == 0, ("hipExtModuleLaunchKernel", rc)
+    hip.hipGetErrorString.restype = ctypes.c_char_p
+    assert rc == 0, ("hipExtModuleLaunchKernel", rc, hip.hipGetErrorString(rc))
 section()  # warm-up, stopped: nothing recorded
 torch.cuda.synchronize()
 c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
@@ -243,10 +243,10 @@ print("RESULT " + json.dumps({"stats": stats, "available": cupti.capture_availab
 """.replace("PROBE", repr(PROBE))
 
 
-def test_runtime_copies_and_fills_are_not_kernels_and_partial_blocks_count():
+def test_runtime_copies_and_fills_are_not_kernels():
     """CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL only (CuptiProfiler.cpp:118, 179): a section of
-    copy_ + hipMemsetAsync + two kernels yields exactly the two kernels' keys; gridX counts the
-    partial last block of a global size of 1000 over 256-wide workgroups (:182-185)."""
+    copy_ + hipMemsetAsync + two kernels (one launched through the module / ext API with its
+    global size in work-items) yields exactly the two kernels' keys (:182-185)."""
     assert os.path.exists(PROBE), "build tests/native first (__graft_entry__.build())"
     out = _child(RUNTIME)
     assert out["available"]

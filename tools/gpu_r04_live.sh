@@ -3,14 +3,14 @@
 # buffer vs callback_counted (the default) at profiling_interval 1 and 16, interleaved twice on
 # one box; gpurun_out/r04_live/
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r04_live
+OUT=$R/gpurun_out/r04_live${TAG}
 mkdir -p "$OUT"
 cd "$R"
 export MASTER_ADDR=127.0.0.1 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0
 port=29571
-for rep in 1 2; do
-  for dl in buffer callback_counted; do
-    for pi in 1 16; do
+for rep in $(seq 1 ${REPS:-2}); do
+  for dl in ${DELIVERIES:-buffer callback_counted}; do
+    for pi in ${INTERVALS:-1 16}; do
       NVRX_CAPTURE_DELIVERY=$dl MASTER_PORT=$port timeout -k 10 240 python -u tools/live_gpt2.py --batch 8 --profiling-interval $pi \
           --steps 64 --report-every 32 --base-steps 30 --out "$OUT/r${rep}_${dl}_pi$pi.json" > "$OUT/r${rep}_${dl}_pi$pi.log" 2>&1 || { echo "fail $rep $dl $pi"; tail -5 "$OUT/r${rep}_${dl}_pi$pi.log"; exit 1; }
       port=$((port+1))

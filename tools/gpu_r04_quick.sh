@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/r04_quick${TAG}
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -v --timeout 300 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest.log" 2>&1
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -v --timeout 170 --timeout-method thread ${PYTEST_ARGS} > "$OUT/pytest.log" 2>&1
 rc=$?
 tail -15 "$OUT/pytest.log"
 [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
