@@ -23,7 +23,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <mutex>
 
 #include "segment_kernels.h"
 
@@ -410,8 +409,8 @@ int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
 
 // dynamic LDS of a bucketing launch: a single workgroup may take the whole 160 KiB of a CU
 // (MI355X_MICROARCH.md), less the kernel's few static bytes.  NVRX_RB_LDS_KB (a build-time
-// tuning constant) caps it lower, so that class-kernel blocks fit beside a bucketing block
-// (records_stats' pipelined chunks, below).
+// tuning constant) caps it lower (round 4's variants that left class-kernel blocks room beside a
+// bucketing block: slower, profiles/r04/zipf_ab/).
 #ifndef NVRX_RB_LDS_KB
 #define NVRX_RB_LDS_KB 160
 #endif
@@ -511,35 +510,6 @@ hipError_t records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64
                                 seg_len, out_ns, counts, st, tiny);
 }
 
-// Pipelined record statistics (NVRX_RS_CHUNKS > 1, a build-time constant): the streams are
-// bucketed in chunks on the caller's stream while the class kernels of the previous chunk run on
-// a second one, so that class-kernel blocks share the CUs with a bucketing block (which then
-// must leave them room: NVRX_RB_WAVES / NVRX_RB_LDS_KB).
-#ifndef NVRX_RS_CHUNKS
-#define NVRX_RS_CHUNKS 1
-#endif
-struct RsPipe {
-    hipStream_t side = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-};
-static hipError_t rs_pipe(RsPipe*& out) {
-    static RsPipe* pipes[64] = {nullptr};
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    int dev = 0;
-    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
-    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    if (!pipes[dev]) {
-        RsPipe* p = new RsPipe{};
-        hipError_t e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
-        for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&p->ev[i], hipEventDisableTiming);
-        if (e != hipSuccess) return e;
-        pipes[dev] = p;
-    }
-    out = pipes[dev];
-    return hipSuccess;
-}
-
 // Whole record-stream report statistics: bucketing (which reduces the staged buckets of <=
 // RB_TINY records itself), then length-classed statistics of every other bucket; col_ref by a
 // column reduction (cheaper than per-segment atomics once there are many streams).
@@ -547,41 +517,16 @@ hipError_t records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_
                          int64_t nslots, int64_t cap, int mode, int64_t max_len, int64_t* seg_off,
                          int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
                          const nvrx_stats_soa& out, uint32_t* col_ref, hipStream_t st) {
-    const int64_t keep = std::max<int64_t>(1, (cap > 0 && max_len > cap) ? cap : max_len);
-    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
-    if (hipError_t e = hipStreamIsCapturing(st, &cst); e != hipSuccess) return e;
-    const int64_t chunks = std::min<int64_t>(NVRX_RS_CHUNKS, nstreams);
-    if (chunks <= 1 || cst != hipStreamCaptureStatusNone) {
-        hipError_t e = records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off, seg_len, out_ns,
-                                      counts, st, &out);
-        if (e != hipSuccess) return e;
-        e = segment_stats_ragged(out_ns, seg_off, seg_len, nstreams * nslots, keep, 0, mode, true, out,
-                                 nullptr, 0, st);
-        if (e != hipSuccess || !col_ref) return e;
-        return kernel_ref(out.num, out.med, nstreams, nslots, nullptr, col_ref, st);
-    }
-    RsPipe* pp = nullptr;
-    if (hipError_t e = rs_pipe(pp); e != hipSuccess) return e;
-    hipError_t e = hipSuccess;
-    for (int64_t c = 0; c < chunks && e == hipSuccess; ++c) {
-        const int64_t t0 = nstreams * c / chunks, t1 = nstreams * (c + 1) / chunks;
-        e = records_bucket_range(recs, rec_off, t0, t1 - t0, nstreams, nslots, cap, 0, seg_off, seg_len,
-                                 out_ns, counts, st, &out);
-        if (e == hipSuccess) e = hipEventRecord(pp->ev[0], st);
-        if (e == hipSuccess) e = hipStreamWaitEvent(pp->side, pp->ev[0], 0);
-        if (e != hipSuccess) break;
-        const int64_t g0 = t0 * nslots;
-        const nvrx_stats_soa o{out.num + g0, out.min + g0, out.max + g0, out.med + g0, out.avg + g0,
-                               out.std + g0};
-        e = segment_stats_ragged(out_ns, seg_off + g0, seg_len + g0, (t1 - t0) * nslots, keep, 0, mode,
-                                 true, o, nullptr, 0, pp->side);
-    }
-    // joined on every path
-    const hipError_t j1 = hipEventRecord(pp->ev[1], pp->side);
-    const hipError_t j2 = j1 == hipSuccess ? hipStreamWaitEvent(st, pp->ev[1], 0) : j1;
+    // (round 4 measured bucketing stream chunks while the previous chunk's class kernels ran on
+    // a second stream, with and without a smaller bucketing block to make room for them: 4.57-5.43
+    // against 4.15-4.17 ms, profiles/r04/zipf_ab/)
+    hipError_t e = records_bucket(recs, rec_off, nstreams, nslots, cap, 0, seg_off, seg_len, out_ns,
+                                  counts, st, &out);
     if (e != hipSuccess) return e;
-    if (j2 != hipSuccess) return j2;
-    if (!col_ref) return hipSuccess;
+    const int64_t keep = std::max<int64_t>(1, (cap > 0 && max_len > cap) ? cap : max_len);
+    e = segment_stats_ragged(out_ns, seg_off, seg_len, nstreams * nslots, keep, 0, mode, true, out,
+                             nullptr, 0, st);
+    if (e != hipSuccess || !col_ref) return e;
     return kernel_ref(out.num, out.med, nstreams, nslots, nullptr, col_ref, st);
 }
 

@@ -190,65 +190,6 @@ void seg_stats_lane_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
     }
 }
 
-// Lane classes with a wave-cooperative load (NVRX_LANE_TILE, a build-time A/B constant): a
-// wave takes 64 consecutive list entries, loads their (16-B aligned) runs with N/4 lanes per
-// segment -- each load instruction covers 64/(N/4) whole runs instead of one 16-B piece of 64
-// different runs -- into an LDS tile, then every lane reads its own run back and reduces it as
-// seg_stats_lane_kernel does.
-#ifndef NVRX_LANE_TILE
-#define NVRX_LANE_TILE 0
-#endif
-template <int N>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LaneOcc<N>::W)))
-void seg_stats_lane_tile_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
-                                nvrx_stats_soa out) {
-    static_assert(N >= 16 && N <= 64, "tile kernel: N in [16, 64]");
-    constexpr int Q = N / 4;      // 16-byte quads per run
-    constexpr int ROW = Q + 1;    // padded LDS row (quads): rows start in different banks
-    constexpr int SPI = 64 / Q;   // runs per load instruction
-    const ColRef cr{nullptr, nullptr, 1, 1.0};
-    __shared__ u32x4 tile[4][64 * ROW];
-    const int wave = threadIdx.x >> 6, lane = lane_id();
-    u32x4* t = tile[wave];
-    const uint32_t start = cls[0], cnt = cls[1];
-    const uint32_t W = gridDim.x * 4u;
-    for (uint32_t t0 = (blockIdx.x * 4u + (uint32_t)wave) * 64u; t0 < cnt; t0 += W * 64u) {
-        int64_t s = -1;
-        const uint32_t* p = nullptr;
-        int n = 0;
-        if (t0 + lane < cnt) {
-            s = list[start + t0 + lane];
-            segs.get(s, p, n);
-        }
-        const int plo = (int)(uint32_t)(uintptr_t)p, phi = (int)(uint32_t)((uintptr_t)p >> 32);
-        u32x4 w[Q];
-#pragma unroll
-        for (int k = 0; k < Q; ++k) {  // all loads in flight before the first LDS store
-            const int j = k * SPI + lane / Q, q = lane % Q;
-            const uint32_t lo = (uint32_t)__shfl(plo, j), hi = (uint32_t)__shfl(phi, j);
-            const int nj = __shfl(n, j);
-            const u32x4* pj = (const u32x4*)(((uint64_t)hi << 32) | lo);
-            w[k] = 4 * q < nj ? pj[q] : u32x4{~0u, ~0u, ~0u, ~0u};
-        }
-#pragma unroll
-        for (int k = 0; k < Q; ++k) t[(k * SPI + lane / Q) * ROW + lane % Q] = w[k];
-        __builtin_amdgcn_wave_barrier();
-        if (s >= 0) {
-            unsigned v[N];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                const u32x4 x = t[lane * ROW + q];
-                v[4 * q + 0] = x.x;
-                v[4 * q + 1] = x.y;
-                v[4 * q + 2] = x.z;
-                v[4 * q + 3] = x.w;
-            }
-            lane_stats<N, LaneMin<N>::n>(v, n, s, out, cr);
-        }
-        __builtin_amdgcn_wave_barrier();  // the tile is reused
-    }
-}
-
 // ---------------------------------------------------------------- wave / workgroup classes
 // One wave per segment over a class list.  Waves take chunks of CH consecutive list
 // entries (static round robin; CH shrinks when the class is small so every wave gets
@@ -456,14 +397,6 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
 template <int N>
 void launch_lane(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls, bool aligned16,
                  const nvrx_stats_soa& out, hipStream_t st) {
-    if constexpr (NVRX_LANE_TILE && N >= 16 && N <= 64) {
-        if (aligned16) {
-            const unsigned blocks = (unsigned)(cu_count() * 2 * LaneOcc<N>::W);
-            hipLaunchKernelGGL((seg_stats_lane_tile_kernel<N>), dim3(blocks), dim3(256), 0, st, segs, list,
-                               cls, out);
-            return;
-        }
-    }
     const unsigned blocks = (unsigned)(cu_count() * 2 * LaneOcc<N>::W);
     hipLaunchKernelGGL((seg_stats_lane_kernel<N>), dim3(blocks), dim3(256), 0, st, segs, list, cls,
                        aligned16 ? 1 : 0, out);
