@@ -39,7 +39,8 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 
 // Timing-only ablation builds (tools/build_variant.sh -DNVRX_RB_ABLATE=k; outputs are wrong):
 // 1 = stop after pass 1 + the scans, 2 = also skip the staged copy-out and the tiny statistics
-// after pass 2, 3 = skip only the tiny statistics.  0 (the library): the whole kernel.
+// after pass 2, 3 = skip only the tiny statistics, 4 = pass 1's loads without the LDS slot counts,
+// then stop.  0 (the library): the whole kernel.
 #ifndef NVRX_RB_ABLATE
 #define NVRX_RB_ABLATE 0
 #endif
@@ -54,7 +55,10 @@ constexpr int RB_TINY = 8;  // records_stats: buckets this short are reduced by 
 // records [lo, hi) of a stream in 16-byte pairs where the base allows it; f(rec) per record.
 // RB_UNROLL independent loads per lane are issued before any is consumed: a wave keeps
 // RB_UNROLL KB in flight instead of one (the loop is otherwise latency-bound).
-constexpr int RB_UNROLL = 8;
+#ifndef NVRX_RB_UNROLL  // build-time tuning constant
+#define NVRX_RB_UNROLL 8
+#endif
+constexpr int RB_UNROLL = NVRX_RB_UNROLL;
 template <class F>
 __device__ __forceinline__ void for_records(const nvrx_record* rs, int64_t lo, int64_t hi, int lane,
                                             bool pairs, F&& f) {
@@ -168,9 +172,13 @@ void records_bucket_kernel(
     }
     if (threadIdx.x == 0) any_ovf = force_stable ? 1u : 0u;
     __syncthreads();
+    uint32_t sink = 0;  // NVRX_RB_ABLATE == 4: the records consumed without the LDS counts
     const auto count = [&](const nvrx_record& r) {
         const uint32_t ls = r.slot - slot_lo;  // this pass's slots: [slot_lo, slot_lo + nslots)
-        if (ls < (uint32_t)nslots) atomicAdd(&cnt[ls], 1u);
+        if (NVRX_RB_ABLATE == 4)
+            sink += ls;
+        else if (ls < (uint32_t)nslots)
+            atomicAdd(&cnt[ls], 1u);
     };
     if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
 #pragma unroll
@@ -279,6 +287,10 @@ void records_bucket_kernel(
     }
     __syncthreads();
     if (NVRX_RB_ABLATE == 1) return;
+    if (NVRX_RB_ABLATE == 4) {
+        if (sink == 0x12345u) counts[0] = (int32_t)sink;  // keeps the loads alive
+        return;
+    }
     // positions below stage_lim go to LDS (cold buckets only: an overflowed slot's walk
     // writes to memory directly)
     const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
