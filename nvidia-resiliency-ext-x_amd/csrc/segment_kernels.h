@@ -1144,8 +1144,11 @@ static_assert(NVRX_LEAN_GROUP_MAX >= 1 && NVRX_LEAN_GROUP_MAX <= 64, "NVRX_LEAN_
 #ifndef NVRX_LEAN_GROUP_PL_MAX  // FULL segments of up to 64 * this many samples take the group kernel
 #define NVRX_LEAN_GROUP_PL_MAX 128
 #endif
+#ifndef NVRX_LEAN_GROUP_WAVES  // build-time tuning constant: the fewest waves a grouped grid keeps
+#define NVRX_LEAN_GROUP_WAVES 32768
+#endif
 static inline int lean_group(int64_t nseg) {
-    const int64_t g = nseg / 32768;
+    const int64_t g = nseg / NVRX_LEAN_GROUP_WAVES;
     return g < 1 ? 1 : g > NVRX_LEAN_GROUP_MAX ? NVRX_LEAN_GROUP_MAX : (int)g;
 }
 
