@@ -40,7 +40,7 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 // Timing-only ablation builds (tools/build_variant.sh -DNVRX_RB_ABLATE=k; outputs are wrong):
 // 1 = stop after pass 1 + the scans, 2 = also skip the staged copy-out and the tiny statistics
 // after pass 2, 3 = skip only the tiny statistics, 4 = pass 1's loads without the LDS slot counts,
-// then stop.  0 (the library): the whole kernel.
+// then stop, 5 = pass 1 alone (no scans).  0 (the library): the whole kernel.
 #ifndef NVRX_RB_ABLATE
 #define NVRX_RB_ABLATE 0
 #endif
@@ -201,6 +201,10 @@ void records_bucket_kernel(
     }
     for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, count);
     __syncthreads();
+    if (NVRX_RB_ABLATE == 5) {  // pass 1 alone (no scans)
+        if (threadIdx.x == 0 && cnt[0] == 0x12345u) counts[0] = 1;
+        return;
+    }
 
     // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
     // block's other waves would otherwise wait at the barrier while one wave walks all the

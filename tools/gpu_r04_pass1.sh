@@ -4,11 +4,11 @@
 # loads in flight per lane for the stream's tail) -- and the full kernel with 16 (u16) against the
 # library; interleaved twice.  Output: gpurun_out/r04_pass1/
 R=$GRAFT_REPO_ROOT
-OUT=$R/gpurun_out/r04_pass1
+OUT=$R/gpurun_out/r04_pass1${TAG}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for round in 1 2; do
-  for v in tree abl1 abl4 abl1u16 u16; do
+  for v in ${VARIANTS:-tree abl1 abl4 abl1u16 u16}; do
     if [ $v = tree ]; then PKG=$R/nvidia-resiliency-ext-x_amd; else PKG=$R/tools/ab_$v; fi
     AB_PKG=$PKG timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/${v}_$round" -o t -- python3 "$R/tools/ab_zipf.py" 10 > "$OUT/${v}_$round.log" 2>&1 || exit 1
