@@ -44,16 +44,6 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 #ifndef NVRX_RB_ABLATE
 #define NVRX_RB_ABLATE 0
 #endif
-// RB_PERSIST (build-time): one block per CU walks its streams, prefetching the next stream's
-// register-held head while the current stream's buckets are written out (see the kernel)
-#ifndef NVRX_RB_PERSIST
-#define NVRX_RB_PERSIST 0
-#endif
-constexpr bool RB_PERSIST = NVRX_RB_PERSIST != 0;
-#ifndef NVRX_RB_PREFETCH  // register pairs per lane prefetched (RB_PERSIST): the rest load as before
-#define NVRX_RB_PREFETCH 8
-#endif
-static_assert(!(NVRX_RB_PERSIST && NVRX_RB_ABLATE), "ablation builds time the one-stream-per-block kernel");
 
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
 // Slots one bucketing pass counts in LDS; a larger slot table is bucketed in passes over
@@ -130,7 +120,7 @@ void records_bucket_kernel(
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
     int32_t* counts, int64_t stash_pairs, int64_t stage_cap, uint32_t cold_max,
     nvrx_stats_soa tiny, uint32_t slot_lo, int64_t seg_stride, int pass, int64_t t0,
-    int64_t nstreams_total, int64_t tend) {
+    int64_t nstreams_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
@@ -143,320 +133,289 @@ void records_bucket_kernel(
     u32x4* stash = (u32x4*)(stage + stage_cap);
     __shared__ uint32_t any_ovf;
     __shared__ uint32_t wtot[3][RB_WAVES];
+    const int64_t t = t0 + blockIdx.x;  // this launch's streams: [t0, t0 + gridDim.x)
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
+    const int64_t r0 = rec_off[t], r1 = rec_off[t + 1];
+    const nvrx_record* rs = recs + r0;
+    const int64_t n = r1 - r0;
+    const int64_t base = stream_base(rec_off, t, nslots);
     // a slot table larger than one pass's LDS counters: pass p's buckets follow the regions of
     // passes 0..p-1, each as large as records_bucket_capacity's per-pass term
     const int64_t ns_off = pass == 0 ? 0 :
         (int64_t)pass * (((rec_off[nstreams_total] + 3) & ~(int64_t)3) + nstreams_total * stream_slack(RB_PASS_SLOTS));
+    const bool pairs = (((uintptr_t)rs) & 15) == 0;
+    // The head of the stream -- up to RB_REGS x 64 x RB_WAVES record pairs -- is held in
+    // registers between the passes, the waves sweeping it together (pair (u RB_WAVES + w) 64 +
+    // lane in register u of wave w: 1.36 against 1.45 ms for per-wave chunks in the pass-1
+    // skeleton on configs[3], tools/mb_rb_read.hip); the rest of the stream is split into
+    // per-wave chunks whose heads go to the LDS stash.
+    const int64_t rp = pairs ? min(n >> 1, (int64_t)RB_REGS * 64 * RB_WAVES) : 0;  // register pairs
+    const u32x4* q = (const u32x4*)rs;
+    // wave w's chunk of the rest: [lo, hi), even boundaries
+    const int64_t n_rest = n - 2 * rp;
+    const int64_t per = ((n_rest + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
+    const int64_t lo = 2 * rp + min(n_rest, per * wave), hi = min(n, lo + per);
+    const bool wpairs = pairs && ((hi - lo) % 2 == 0);
+    // pairs of this wave's chunk held in LDS between the passes (0 when not pair-aligned)
+    const int64_t snp = wpairs ? min((hi - lo) >> 1, stash_pairs) : 0;
+    u32x4* wstash = stash + wave * stash_pairs;
+    const u32x4* wq = (const u32x4*)(rs + lo);
+    // pairs [held, np) of the chunk are read again in pass 2
+    const int64_t np = wpairs ? (hi - lo) >> 1 : 0;
+    const int64_t held = snp;
     u32x4 reg[RB_REGS > 0 ? RB_REGS : 1];
-    constexpr int RB_PF = NVRX_RB_PREFETCH < RB_REGS ? NVRX_RB_PREFETCH : RB_REGS;
-    bool prefetched = false;  // reg[] already holds (or is loading) this stream's head
-    // streams t0 + blockIdx.x, + gridDim.x, ... below tend: one per block, or (RB_PERSIST) a
-    // block per CU walking its streams, the next stream's head loads in flight while the current
-    // stream's buckets are written out
-    for (int64_t t = t0 + blockIdx.x; t < tend; t += gridDim.x) {
-        const int64_t r0 = rec_off[t], r1 = rec_off[t + 1];
-        const nvrx_record* rs = recs + r0;
-        const int64_t n = r1 - r0;
-        const int64_t base = stream_base(rec_off, t, nslots);
-        const bool pairs = (((uintptr_t)rs) & 15) == 0;
-        // The head of the stream -- up to RB_REGS x 64 x RB_WAVES record pairs -- is held in
-        // registers between the passes, the waves sweeping it together (pair (u RB_WAVES + w) 64 +
-        // lane in register u of wave w: 1.36 against 1.45 ms for per-wave chunks in the pass-1
-        // skeleton on configs[3], tools/mb_rb_read.hip); the rest of the stream is split into
-        // per-wave chunks whose heads go to the LDS stash.
-        const int64_t rp = pairs ? min(n >> 1, (int64_t)RB_REGS * 64 * RB_WAVES) : 0;  // register pairs
-        const u32x4* q = (const u32x4*)rs;
-        // wave w's chunk of the rest: [lo, hi), even boundaries
-        const int64_t n_rest = n - 2 * rp;
-        const int64_t per = ((n_rest + RB_WAVES - 1) / RB_WAVES + 1) & ~(int64_t)1;
-        const int64_t lo = 2 * rp + min(n_rest, per * wave), hi = min(n, lo + per);
-        const bool wpairs = pairs && ((hi - lo) % 2 == 0);
-        // pairs of this wave's chunk held in LDS between the passes (0 when not pair-aligned)
-        const int64_t snp = wpairs ? min((hi - lo) >> 1, stash_pairs) : 0;
-        u32x4* wstash = stash + wave * stash_pairs;
-        const u32x4* wq = (const u32x4*)(rs + lo);
-        // pairs [held, np) of the chunk are read again in pass 2
-        const int64_t np = wpairs ? (hi - lo) >> 1 : 0;
-        const int64_t held = snp;
 
-        if (RB_PERSIST) __syncthreads();  // the previous stream's users of the LDS are done
-        for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
-            cnt[s] = 0u;
-            cur[s] = 0u;
-        }
-        if (threadIdx.x == 0) any_ovf = force_stable ? 1u : 0u;
-        __syncthreads();
-        uint32_t sink = 0;  // NVRX_RB_ABLATE == 4: the records consumed without the LDS counts
-        const auto count = [&](const nvrx_record& r) {
-            const uint32_t ls = r.slot - slot_lo;  // this pass's slots: [slot_lo, slot_lo + nslots)
-            if (NVRX_RB_ABLATE == 4)
-                sink += ls;
-            else if (ls < (uint32_t)nslots)
-                atomicAdd(&cnt[ls], 1u);
-        };
-        if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
+    for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
+        cnt[s] = 0u;
+        cur[s] = 0u;
+    }
+    if (threadIdx.x == 0) any_ovf = force_stable ? 1u : 0u;
+    __syncthreads();
+    uint32_t sink = 0;  // NVRX_RB_ABLATE == 4: the records consumed without the LDS counts
+    const auto count = [&](const nvrx_record& r) {
+        const uint32_t ls = r.slot - slot_lo;  // this pass's slots: [slot_lo, slot_lo + nslots)
+        if (NVRX_RB_ABLATE == 4)
+            sink += ls;
+        else if (ls < (uint32_t)nslots)
+            atomicAdd(&cnt[ls], 1u);
+    };
+    if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
 #pragma unroll
-            for (int u = 0; u < RB_REGS; ++u) {
-                const int64_t p = ((int64_t)u * RB_WAVES + wave) * 64 + lane;
-                if (prefetched && u < RB_PF) continue;  // already in flight
-                reg[u] = p < rp ? __builtin_nontemporal_load(q + p) : u32x4{~0u, 0u, ~0u, 0u};
-            }
+        for (int u = 0; u < RB_REGS; ++u) {
+            const int64_t p = ((int64_t)u * RB_WAVES + wave) * 64 + lane;
+            reg[u] = p < rp ? __builtin_nontemporal_load(q + p) : u32x4{~0u, 0u, ~0u, 0u};
         }
-        for_pairs(wq, 0, snp, lane, [&](const u32x4& w, int64_t p) {
-            wstash[p] = w;
-            count(nvrx_record{w.x, w.y});
-            count(nvrx_record{w.z, w.w});
-        });
-        if (RB_REGS > 0) {
+    }
+    for_pairs(wq, 0, snp, lane, [&](const u32x4& w, int64_t p) {
+        wstash[p] = w;
+        count(nvrx_record{w.x, w.y});
+        count(nvrx_record{w.z, w.w});
+    });
+    if (RB_REGS > 0) {
 #pragma unroll
-            for (int u = 0; u < RB_REGS; ++u) {
-                count(nvrx_record{reg[u].x, reg[u].y});
-                count(nvrx_record{reg[u].z, reg[u].w});
-            }
+        for (int u = 0; u < RB_REGS; ++u) {
+            count(nvrx_record{reg[u].x, reg[u].y});
+            count(nvrx_record{reg[u].z, reg[u].w});
         }
-        for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, count);
-        __syncthreads();
-        if (NVRX_RB_ABLATE == 5) {  // pass 1 alone (no scans)
-            if (threadIdx.x == 0 && cnt[0] == 0x12345u) counts[0] = 1;
-            return;
-        }
+    }
+    for_records(rs, lo + 2 * (wpairs ? held : 0), hi, lane, wpairs, count);
+    __syncthreads();
+    if (NVRX_RB_ABLATE == 5) {  // pass 1 alone (no scans)
+        if (threadIdx.x == 0 && cnt[0] == 0x12345u) counts[0] = 1;
+        return;
+    }
 
-        // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
-        // block's other waves would otherwise wait at the barrier while one wave walks all the
-        // slots: with one block per CU that wait was ~1 ms of configs[3]):
-        //   (a) chunk totals -> LDS, (b) each wave scans its chunk from the preceding totals.
-        // With staging the bucket array is laid out by tier, slot order inside a tier: the tiny
-        // buckets (<= RB_TINY records), the other cold ones (<= cold_max, not overflowed), then
-        // the rest -- one scan per tier, each carried past the tiers before it.  The first
-        // stage_cap positions (tiny and cold buckets) are assembled in LDS and written out with
-        // 16-byte stores; see records_bucket for what pays.
-        const auto keep_of = [&](uint32_t total) {
-            return (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
-        };
-        const bool staging = stage_cap > 0 && !force_stable;
-        const auto tier_of = [&](uint32_t total) {
-            const uint32_t keep = keep_of(total);
-            if (!staging || keep != total || keep > cold_max) return 2;
-            return keep <= (uint32_t)RB_TINY ? 0 : 1;
-        };
-        const int64_t chunk = ((nslots + RB_WAVES - 1) / RB_WAVES + 63) & ~(int64_t)63;
-        const int64_t c_lo = min(nslots, chunk * wave), c_hi = min(nslots, c_lo + chunk);
-        {
-            uint32_t p0 = 0, p1 = 0, p2 = 0;
-            for (int64_t s = c_lo + lane; s < c_hi; s += 64) {
-                const uint32_t total = cnt[s];
-                const uint32_t padded = (keep_of(total) + 3u) & ~3u;
-                const int tr = tier_of(total);
-                p0 += tr == 0 ? padded : 0u;
-                p1 += tr == 1 ? padded : 0u;
-                p2 += tr == 2 ? padded : 0u;
-            }
-            p0 = wave_sum_u32(p0);
-            p1 = wave_sum_u32(p1);
-            p2 = wave_sum_u32(p2);
-            if (lane == 0) {
-                wtot[0][wave] = p0;
-                wtot[1][wave] = p1;
-                wtot[2][wave] = p2;
-            }
+    // exclusive scan of padded keeps over slots, every wave on its own chunk of slots (the
+    // block's other waves would otherwise wait at the barrier while one wave walks all the
+    // slots: with one block per CU that wait was ~1 ms of configs[3]):
+    //   (a) chunk totals -> LDS, (b) each wave scans its chunk from the preceding totals.
+    // With staging the bucket array is laid out by tier, slot order inside a tier: the tiny
+    // buckets (<= RB_TINY records), the other cold ones (<= cold_max, not overflowed), then
+    // the rest -- one scan per tier, each carried past the tiers before it.  The first
+    // stage_cap positions (tiny and cold buckets) are assembled in LDS and written out with
+    // 16-byte stores; see records_bucket for what pays.
+    const auto keep_of = [&](uint32_t total) {
+        return (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+    };
+    const bool staging = stage_cap > 0 && !force_stable;
+    const auto tier_of = [&](uint32_t total) {
+        const uint32_t keep = keep_of(total);
+        if (!staging || keep != total || keep > cold_max) return 2;
+        return keep <= (uint32_t)RB_TINY ? 0 : 1;
+    };
+    const int64_t chunk = ((nslots + RB_WAVES - 1) / RB_WAVES + 63) & ~(int64_t)63;
+    const int64_t c_lo = min(nslots, chunk * wave), c_hi = min(nslots, c_lo + chunk);
+    {
+        uint32_t p0 = 0, p1 = 0, p2 = 0;
+        for (int64_t s = c_lo + lane; s < c_hi; s += 64) {
+            const uint32_t total = cnt[s];
+            const uint32_t padded = (keep_of(total) + 3u) & ~3u;
+            const int tr = tier_of(total);
+            p0 += tr == 0 ? padded : 0u;
+            p1 += tr == 1 ? padded : 0u;
+            p2 += tr == 2 ? padded : 0u;
         }
-        __syncthreads();
-        uint32_t cold_total = 0;
-        {
-            uint32_t tiny_total = 0;
-            for (int w = 0; w < RB_WAVES; ++w) {
-                tiny_total += wtot[0][w];
-                cold_total += wtot[0][w] + wtot[1][w];
-            }
-            const uint32_t lim = (uint32_t)min((int64_t)cold_total, stage_cap);
-            bool overflow = false;
+        p0 = wave_sum_u32(p0);
+        p1 = wave_sum_u32(p1);
+        p2 = wave_sum_u32(p2);
+        if (lane == 0) {
+            wtot[0][wave] = p0;
+            wtot[1][wave] = p1;
+            wtot[2][wave] = p2;
+        }
+    }
+    __syncthreads();
+    uint32_t cold_total = 0;
+    {
+        // the tier totals and this wave's carries from the waves' chunk totals: lane w reads
+        // wave w's, one wave reduction each (a serial walk over the waves' totals, 16 dependent
+        // LDS reads for the last wave and each tier, was ~1/3 of the scan phase)
+        const uint32_t w0 = lane < RB_WAVES ? wtot[0][lane] : 0u;
+        const uint32_t w1 = lane < RB_WAVES ? wtot[1][lane] : 0u;
+        const uint32_t w2 = lane < RB_WAVES ? wtot[2][lane] : 0u;
+        const uint32_t tiny_total = wave_sum_u32(w0);
+        cold_total = tiny_total + wave_sum_u32(w1);
+        const uint32_t lim = (uint32_t)min((int64_t)cold_total, stage_cap);
+        bool overflow = false;
 #pragma unroll 1
-            for (int k = 0; k < 3; ++k) {  // one tier at a time: one scan's registers live
-                uint32_t carry = k == 0 ? 0u : k == 1 ? tiny_total : cold_total;
-                for (int w = 0; w < wave; ++w) carry += wtot[k][w];
-                for (int64_t c = c_lo; c < c_hi; c += 64) {
-                    const int64_t s = c + lane;
-                    uint32_t keep = 0, total = 0;
-                    bool mine = false;
-                    if (s < c_hi) {
-                        total = cnt[s];
-                        keep = keep_of(total);
-                        mine = tier_of(total) == k;
-                    }
-                    const uint32_t padded = mine ? (keep + 3u) & ~3u : 0u;
-                    const uint32_t incl = wave_incl_scan_u32(padded);
-                    if (mine) {
-                        const uint32_t st = carry + incl - padded;
-                        const bool ovf = keep != total;
-                        overflow |= ovf;
-                        const uint32_t flag = ovf || force_stable ? RB_OVF : 0u;
-                        start[s] = st | flag;
-                        cur[s] = flag ? RB_OVF : st;  // pass 2's write cursor (absolute in the stream)
-                        const int64_t g = t * seg_stride + slot_lo + s;
-                        seg_off[g] = ns_off + base + st;
-                        // a bucket this kernel reduces itself (after pass 2): a negative length
-                        const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
-                        seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
-                        counts[g] = (int32_t)total;
-                    }
-                    carry += __builtin_amdgcn_readlane(incl, 63);
+        for (int k = 0; k < 3; ++k) {  // one tier at a time: one scan's registers live
+            const uint32_t wk = k == 0 ? w0 : k == 1 ? w1 : w2;
+            uint32_t carry = (k == 0 ? 0u : k == 1 ? tiny_total : cold_total) +
+                             wave_sum_u32(lane < wave ? wk : 0u);
+            for (int64_t c = c_lo; c < c_hi; c += 64) {
+                const int64_t s = c + lane;
+                uint32_t keep = 0, total = 0;
+                bool mine = false;
+                if (s < c_hi) {
+                    total = cnt[s];
+                    keep = keep_of(total);
+                    mine = tier_of(total) == k;
                 }
+                const uint32_t padded = mine ? (keep + 3u) & ~3u : 0u;
+                const uint32_t incl = wave_incl_scan_u32(padded);
+                if (mine) {
+                    const uint32_t st = carry + incl - padded;
+                    const bool ovf = keep != total;
+                    overflow |= ovf;
+                    const uint32_t flag = ovf || force_stable ? RB_OVF : 0u;
+                    start[s] = st | flag;
+                    cur[s] = flag ? RB_OVF : st;  // pass 2's write cursor (absolute in the stream)
+                    const int64_t g = t * seg_stride + slot_lo + s;
+                    seg_off[g] = ns_off + base + st;
+                    // a bucket this kernel reduces itself (after pass 2): a negative length
+                    const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
+                    seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
+                    counts[g] = (int32_t)total;
+                }
+                carry += __builtin_amdgcn_readlane(incl, 63);
             }
-            if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
         }
-        __syncthreads();
-        if (NVRX_RB_ABLATE == 1) return;
-        if (NVRX_RB_ABLATE == 4) {
-            if (sink == 0x12345u) counts[0] = (int32_t)sink;  // keeps the loads alive
-            return;
-        }
-        // positions below stage_lim go to LDS (cold buckets only: an overflowed slot's walk
-        // writes to memory directly)
-        const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
-        uint32_t* out = out_ns + ns_off + base;
+        if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
+    }
+    __syncthreads();
+    if (NVRX_RB_ABLATE == 1) return;
+    if (NVRX_RB_ABLATE == 4) {
+        if (sink == 0x12345u) counts[0] = (int32_t)sink;  // keeps the loads alive
+        return;
+    }
+    // positions below stage_lim go to LDS (cold buckets only: an overflowed slot's walk
+    // writes to memory directly)
+    const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
+    uint32_t* out = out_ns + ns_off + base;
 
-        // records of slots that kept everything: any order.  The cursor starts at the bucket's
-        // start, so a record costs one returning LDS atomic (a lookup of start[] before the atomic
-        // doubled the dependent LDS round trips: 4.5 -> 3.x ms on configs[3]); overflowed slots
-        // hold RB_OVF, which the increments keep set, and are skipped here.
-        const auto place = [&](const nvrx_record& r) {
-            const uint32_t ls = r.slot - slot_lo;
-            if (ls < (uint32_t)nslots) {
-                const uint32_t pos = atomicAdd(&cur[ls], 1u);
-                if (pos < stage_lim)
-                    stage[pos] = r.ns;
-                else if (!(pos & RB_OVF))
-                    out[pos] = r.ns;
-            }
-        };
-        // The stashed head of the chunk (LDS) is placed while each batch of the rest's loads is
-        // in flight: `per_it` stashed pairs per lane between issuing a batch and consuming it.
-        int64_t sp = lane;  // this lane's stash cursor
-        const auto place_stash = [&](int m) {
-            for (int j = 0; j < m && sp < snp; ++j, sp += 64) {
-                const u32x4 w = wstash[sp];
-                place(nvrx_record{w.x, w.y});
-                place(nvrx_record{w.z, w.w});
-            }
-        };
-        const auto place_regs = [&]() {
-#pragma unroll
-            for (int u = 0; u < RB_REGS; ++u) {
-                place(nvrx_record{reg[u].x, reg[u].y});
-                place(nvrx_record{reg[u].z, reg[u].w});
-            }
-        };
-        if (RB_REGS > 0 && !RB_PERSIST) place_regs();  // no memory dependency: they go out first
-        {
-            const int64_t iters = (np - held) / (64 * RB_UNROLL);
-            const int per_it = iters > 0 ? (int)((snp / 64 + iters - 1) / iters) : 0;
-            int64_t i = held + lane;
-            for (; i + 64 * (RB_UNROLL - 1) < np; i += 64 * RB_UNROLL) {
-                u32x4 w[RB_UNROLL];
-#pragma unroll
-                for (int u = 0; u < RB_UNROLL; ++u) w[u] = __builtin_nontemporal_load(wq + i + 64 * u);
-                place_stash(per_it);
-#pragma unroll
-                for (int u = 0; u < RB_UNROLL; ++u) {
-                    place(nvrx_record{w[u].x, w[u].y});
-                    place(nvrx_record{w[u].z, w[u].w});
-                }
-            }
-            for (; i < np; i += 64) {
-                const u32x4 w = wq[i];
-                place(nvrx_record{w.x, w.y});
-                place(nvrx_record{w.z, w.w});
-            }
-            place_stash(1 << 30);
-            // a chunk that is not pair-aligned (np = 0): its records one by one
-            if (!wpairs) for_records(rs, lo, hi, lane, false, place);
+    // records of slots that kept everything: any order.  The cursor starts at the bucket's
+    // start, so a record costs one returning LDS atomic (a lookup of start[] before the atomic
+    // doubled the dependent LDS round trips: 4.5 -> 3.x ms on configs[3]); overflowed slots
+    // hold RB_OVF, which the increments keep set, and are skipped here.
+    const auto place = [&](const nvrx_record& r) {
+        const uint32_t ls = r.slot - slot_lo;
+        if (ls < (uint32_t)nslots) {
+            const uint32_t pos = atomicAdd(&cur[ls], 1u);
+            if (pos < stage_lim)
+                stage[pos] = r.ns;
+            else if (!(pos & RB_OVF))
+                out[pos] = r.ns;
         }
-        prefetched = false;
-        if (RB_REGS > 0 && RB_PERSIST) {
-            // the stream's loads are all consumed: place the register-held head, then issue the next
-            // stream's head into the freed registers -- in flight while this stream's buckets are
-            // written out (no later wait of this stream is on a load, so none waits for them)
-            place_regs();
-            const int64_t tn = t + gridDim.x;
-            if (tn < tend) {
-                const int64_t m0 = rec_off[tn], m1 = rec_off[tn + 1];
-                const u32x4* qn = (const u32x4*)(recs + m0);
-                const int64_t rpn = (((uintptr_t)qn) & 15) == 0 ? min((m1 - m0) >> 1, (int64_t)RB_REGS * 64 * RB_WAVES) : 0;
+    };
+    // The stashed head of the chunk (LDS) is placed while each batch of the rest's loads is
+    // in flight: `per_it` stashed pairs per lane between issuing a batch and consuming it.
+    int64_t sp = lane;  // this lane's stash cursor
+    const auto place_stash = [&](int m) {
+        for (int j = 0; j < m && sp < snp; ++j, sp += 64) {
+            const u32x4 w = wstash[sp];
+            place(nvrx_record{w.x, w.y});
+            place(nvrx_record{w.z, w.w});
+        }
+    };
+    if (RB_REGS > 0) {  // no memory dependency: their atomics and stores go out first
 #pragma unroll
-                for (int u = 0; u < RB_PF; ++u) {
-                    const int64_t p = ((int64_t)u * RB_WAVES + wave) * 64 + lane;
-                    reg[u] = p < rpn ? __builtin_nontemporal_load(qn + p) : u32x4{~0u, 0u, ~0u, 0u};
-                }
-                prefetched = true;
+        for (int u = 0; u < RB_REGS; ++u) {
+            place(nvrx_record{reg[u].x, reg[u].y});
+            place(nvrx_record{reg[u].z, reg[u].w});
+        }
+    }
+    {
+        const int64_t iters = (np - held) / (64 * RB_UNROLL);
+        const int per_it = iters > 0 ? (int)((snp / 64 + iters - 1) / iters) : 0;
+        int64_t i = held + lane;
+        for (; i + 64 * (RB_UNROLL - 1) < np; i += 64 * RB_UNROLL) {
+            u32x4 w[RB_UNROLL];
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) w[u] = __builtin_nontemporal_load(wq + i + 64 * u);
+            place_stash(per_it);
+#pragma unroll
+            for (int u = 0; u < RB_UNROLL; ++u) {
+                place(nvrx_record{w[u].x, w[u].y});
+                place(nvrx_record{w[u].z, w[u].w});
             }
         }
-        if (NVRX_RB_ABLATE == 2) return;
-        if (stage_lim > 0) {  // the assembled head of the bucket array, in 16-byte stores
-            __syncthreads();
-            const u32x4* sv = (const u32x4*)stage;
-            u32x4* ov = (u32x4*)out;  // out = stream base: 16-byte aligned
-            for (uint32_t i = threadIdx.x; i < stage_lim / 4; i += blockDim.x) ov[i] = sv[i];
-            // records_stats: the statistics of the staged buckets of <= RB_TINY records, one lane
-            // per bucket straight from LDS (lane_stats: computeStats bit for bit, as the ragged
-            // lane<8> class does), instead of a later kernel re-reading them through a class list
-            if (tiny.num && NVRX_RB_ABLATE != 3) {
-                for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
-                    const uint32_t total = cnt[s];
-                    const uint32_t keep = keep_of(total);
-                    const uint32_t st = start[s];
-                    if (tier_of(total) == 0 && keep >= 1 && st + ((keep + 3u) & ~3u) <= stage_lim) {
-                        const u32x4 a = sv[st / 4];
-                        const u32x4 b = keep > 4 ? sv[st / 4 + 1] : u32x4{~0u, ~0u, ~0u, ~0u};
-                        unsigned v[RB_TINY] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-                        lane_stats<RB_TINY>(v, (int)keep, t * seg_stride + slot_lo + s, tiny, ColRef{});
-                    }
+        for (; i < np; i += 64) {
+            const u32x4 w = wq[i];
+            place(nvrx_record{w.x, w.y});
+            place(nvrx_record{w.z, w.w});
+        }
+        place_stash(1 << 30);
+        // a chunk that is not pair-aligned (np = 0): its records one by one
+        if (!wpairs) for_records(rs, lo, hi, lane, false, place);
+    }
+    if (NVRX_RB_ABLATE == 2) return;
+    if (stage_lim > 0) {  // the assembled head of the bucket array, in 16-byte stores
+        __syncthreads();
+        const u32x4* sv = (const u32x4*)stage;
+        u32x4* ov = (u32x4*)out;  // out = stream base: 16-byte aligned
+        for (uint32_t i = threadIdx.x; i < stage_lim / 4; i += blockDim.x) ov[i] = sv[i];
+        // records_stats: the statistics of the staged buckets of <= RB_TINY records, one lane
+        // per bucket straight from LDS (lane_stats: computeStats bit for bit, as the ragged
+        // lane<8> class does), instead of a later kernel re-reading them through a class list
+        if (tiny.num && NVRX_RB_ABLATE != 3) {
+            for (int64_t s = threadIdx.x; s < nslots; s += blockDim.x) {
+                const uint32_t total = cnt[s];
+                const uint32_t keep = keep_of(total);
+                const uint32_t st = start[s];
+                if (tier_of(total) == 0 && keep >= 1 && st + ((keep + 3u) & ~3u) <= stage_lim) {
+                    const u32x4 a = sv[st / 4];
+                    const u32x4 b = keep > 4 ? sv[st / 4 + 1] : u32x4{~0u, ~0u, ~0u, ~0u};
+                    unsigned v[RB_TINY] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+                    lane_stats<RB_TINY>(v, (int)keep, t * seg_stride + slot_lo + s, tiny, ColRef{});
                 }
             }
         }
-        if (!any_ovf) {  // (one stream per block: break, so the loop has no back edge)
-            if (RB_PERSIST) continue;
-            break;
+    }
+    if (!any_ovf) return;
+    __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
+    if (wave != 0) return;
+    // the ordered walk counts occurrences of the overflowed slots from zero
+    for (int64_t s = lane; s < nslots; s += 64)
+        if (start[s] & RB_OVF) cur[s] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    // overflowed slots: wave 0 walks the whole stream in push order
+    for (int64_t b = 0; b < n; b += 64) {
+        const int64_t i = b + lane;
+        nvrx_record rec = {0xFFFFFFFFu, 0u};
+        if (i < n) rec = rs[i];
+        rec.slot -= slot_lo;  // this pass's local slot
+        const bool ok = rec.slot < (uint32_t)nslots && (start[rec.slot] & RB_OVF);
+        uint64_t pending = __ballot(ok);
+        uint32_t occ = 0;
+        while (pending) {
+            const int leader = __builtin_ffsll(pending) - 1;
+            const uint32_t ls = __builtin_amdgcn_readlane(rec.slot, leader);
+            const uint64_t grp = __ballot(ok && rec.slot == ls) & pending;
+            const uint32_t c0 = cur[ls];
+            if (ok && rec.slot == ls) occ = c0 + mbcnt(grp);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == leader) cur[ls] = c0 + (uint32_t)__popcll(grp);
+            __builtin_amdgcn_wave_barrier();
+            pending &= ~grp;
         }
-        __syncthreads();  // every wave's pass-2 increments of the RB_OVF cursors are done
-        if (wave != 0) {
-            if (RB_PERSIST) continue;
-            break;
+        if (ok) {
+            const uint32_t total = cnt[rec.slot];
+            const uint32_t keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
+            const uint32_t drop = total - keep;
+            if (occ >= drop) out[(start[rec.slot] & ~RB_OVF) + (occ - drop)] = rec.ns;
         }
-        // the ordered walk counts occurrences of the overflowed slots from zero
-        for (int64_t s = lane; s < nslots; s += 64)
-            if (start[s] & RB_OVF) cur[s] = 0u;
-        __builtin_amdgcn_wave_barrier();
-        // overflowed slots: wave 0 walks the whole stream in push order
-        for (int64_t b = 0; b < n; b += 64) {
-            const int64_t i = b + lane;
-            nvrx_record rec = {0xFFFFFFFFu, 0u};
-            if (i < n) rec = rs[i];
-            rec.slot -= slot_lo;  // this pass's local slot
-            const bool ok = rec.slot < (uint32_t)nslots && (start[rec.slot] & RB_OVF);
-            uint64_t pending = __ballot(ok);
-            uint32_t occ = 0;
-            while (pending) {
-                const int leader = __builtin_ffsll(pending) - 1;
-                const uint32_t ls = __builtin_amdgcn_readlane(rec.slot, leader);
-                const uint64_t grp = __ballot(ok && rec.slot == ls) & pending;
-                const uint32_t c0 = cur[ls];
-                if (ok && rec.slot == ls) occ = c0 + mbcnt(grp);
-                __builtin_amdgcn_wave_barrier();
-                if (lane == leader) cur[ls] = c0 + (uint32_t)__popcll(grp);
-                __builtin_amdgcn_wave_barrier();
-                pending &= ~grp;
-            }
-            if (ok) {
-                const uint32_t total = cnt[rec.slot];
-                const uint32_t keep = (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
-                const uint32_t drop = total - keep;
-                if (occ >= drop) out[(start[rec.slot] & ~RB_OVF) + (occ - drop)] = rec.ns;
-            }
-        }
-        if (!RB_PERSIST) break;
-    }  // streams
+    }
 }
 
 int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
@@ -537,17 +496,10 @@ static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* re
         if (e != hipSuccess) return e;
         attr_lds = lds_launch;
     }
-    int64_t grid = nlaunch;
-    if (RB_PERSIST) {  // one block per CU (the whole LDS each)
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
-            grid = std::min<int64_t>(nlaunch, cus);
-    }
-    hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)grid), dim3(64 * RB_WAVES),
+    hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)nlaunch), dim3(64 * RB_WAVES),
                        lds_launch, st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns,
                        counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa, slot_lo, seg_stride, pass,
-                       t0, nstreams, t0 + nlaunch);
+                       t0, nstreams);
     return hipGetLastError();
 }
 
