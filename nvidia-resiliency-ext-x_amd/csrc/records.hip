@@ -40,7 +40,8 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 // Timing-only ablation builds (tools/build_variant.sh -DNVRX_RB_ABLATE=k; outputs are wrong):
 // 1 = stop after pass 1 + the scans, 2 = also skip the staged copy-out and the tiny statistics
 // after pass 2, 3 = skip only the tiny statistics, 4 = pass 1's loads without the LDS slot counts,
-// then stop, 5 = pass 1 alone (no scans).  0 (the library): the whole kernel.
+// then stop, 5 = pass 1 alone (no scans), 6 = pass 1 + the scan's chunk totals, 7 = pass 1 + the
+// scans without their global stores.  0 (the library): the whole kernel.
 #ifndef NVRX_RB_ABLATE
 #define NVRX_RB_ABLATE 0
 #endif
@@ -246,6 +247,10 @@ void records_bucket_kernel(
         }
     }
     __syncthreads();
+    if (NVRX_RB_ABLATE == 6) {  // pass 1 + the scan's chunk totals only
+        if (threadIdx.x == 0 && wtot[0][0] == 0x12345u) counts[0] = 1;
+        return;
+    }
     uint32_t cold_total = 0;
     {
         // the tier totals and this wave's carries from the waves' chunk totals: lane w reads
@@ -282,11 +287,13 @@ void records_bucket_kernel(
                     start[s] = st | flag;
                     cur[s] = flag ? RB_OVF : st;  // pass 2's write cursor (absolute in the stream)
                     const int64_t g = t * seg_stride + slot_lo + s;
-                    seg_off[g] = ns_off + base + st;
                     // a bucket this kernel reduces itself (after pass 2): a negative length
                     const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
-                    seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
-                    counts[g] = (int32_t)total;
+                    if (NVRX_RB_ABLATE != 7) {  // 7: the scans without their global stores
+                        seg_off[g] = ns_off + base + st;
+                        seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
+                        counts[g] = (int32_t)total;
+                    }
                 }
                 carry += __builtin_amdgcn_readlane(incl, 63);
             }
@@ -294,7 +301,7 @@ void records_bucket_kernel(
         if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
     }
     __syncthreads();
-    if (NVRX_RB_ABLATE == 1) return;
+    if (NVRX_RB_ABLATE == 1 || NVRX_RB_ABLATE == 7) return;
     if (NVRX_RB_ABLATE == 4) {
         if (sink == 0x12345u) counts[0] = (int32_t)sink;  // keeps the loads alive
         return;
