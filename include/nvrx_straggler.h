@@ -226,7 +226,8 @@ int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t
  * nvrx_segment_stats_ragged(aligned16) over the buckets (runs of <= 128 samples bit-exact in
  * every field).  out->* are [nstreams*nslots]; max_len bounds every stream's length
  * (host-known); col_ref (optional, [2*nslots]) as for nvrx_segment_stats_strided (rows =
- * streams), produced by a column reduction.  On return seg_len[g] < 0 marks a bucket of
+ * streams), produced by a column reduction; counts may be NULL here (the pushes per bucket are
+ * then not written: 4 B per (stream, slot) less).  On return seg_len[g] < 0 marks a bucket of
  * -seg_len[g] records whose statistics the bucketing kernel computed itself. */
 int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                        int64_t nslots, int64_t cap, int32_t mode, int64_t max_len, int64_t* seg_off,

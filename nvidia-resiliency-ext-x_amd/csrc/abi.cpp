@@ -207,9 +207,8 @@ int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t 
     NVRX_CHECK_ARG(nstreams >= 0 && nslots >= 0 && max_len >= 0, "nvrx_records_stats: negative size");
     NVRX_CHECK_ARG(out && out->num && out->min && out->max && out->med && out->avg && out->std,
                    "nvrx_records_stats: null output array");
-    NVRX_CHECK_ARG(nstreams == 0 || nslots == 0 ||
-                       (recs && rec_off && seg_off && seg_len && out_ns && counts),
-                   "nvrx_records_stats: null array");
+    NVRX_CHECK_ARG(nstreams == 0 || nslots == 0 || (recs && rec_off && seg_off && seg_len && out_ns),
+                   "nvrx_records_stats: null array");  // counts may be NULL (not written)
     NVRX_CHECK_ARG(mode == NVRX_STATS_FAST || mode == NVRX_STATS_EXACT,
                    "nvrx_records_stats: unknown mode");
     NVRX_CHECK_ARG(nstreams * nslots < (int64_t)1 << 31, "nvrx_records_stats: too many segments");

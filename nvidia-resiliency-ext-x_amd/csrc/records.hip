@@ -298,7 +298,7 @@ void records_bucket_kernel(
                     if (NVRX_RB_ABLATE != 7) {  // 7: the scans without their global stores
                         seg_off[g] = ns_off + base + st;
                         seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
-                        counts[g] = (int32_t)total;
+                        if (counts) counts[g] = (int32_t)total;  // optional in records_stats
                     }
                 }
                 carry0 += __builtin_amdgcn_readlane(i0, 63);

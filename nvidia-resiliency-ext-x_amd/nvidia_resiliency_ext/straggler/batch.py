@@ -144,10 +144,10 @@ class MatrixReporter:
         b = getattr(self, "_bucket", None)
         if b is None or b[2].numel() < need:
             d = self.device
+            # (no per-bucket push counts: a report needs the kept records only)
             b = (torch.empty(self.R * self.K, dtype=torch.int64, device=d),
                  torch.empty(self.R * self.K, dtype=torch.int32, device=d),
-                 torch.empty(max(need, 1), dtype=torch.int32, device=d),
-                 torch.empty(self.R * self.K, dtype=torch.int32, device=d))
+                 torch.empty(max(need, 1), dtype=torch.int32, device=d), None)
             self._bucket = b
         max_len = min(self.cap, n) if self.cap > 0 else n
         self._colref_clean = False

@@ -241,8 +241,9 @@ def records_stats(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: i
                   col_ref: Optional[torch.Tensor] = None, stream=None) -> SegmentStats:
     """Per-(stream, slot) statistics of push-ordered record streams (ring retention of the
     last `cap` + computeStats): bucketing, then the length-classed segment kernels.  `bucket` may pass the
-    (seg_off, seg_len, out_ns, counts) work tensors preallocated; col_ref ([2*nslots] int32)
-    receives the per-slot reference (min over streams of MED | missing)."""
+    (seg_off, seg_len, out_ns, counts) work tensors preallocated (counts may be None: the pushes
+    per bucket are then not written); col_ref ([2*nslots] int32) receives the per-slot reference
+    (min over streams of MED | missing)."""
     nstreams = rec_off.numel() - 1
     dev = recs.device
     n = recs.shape[0]
@@ -259,6 +260,6 @@ def records_stats(recs: torch.Tensor, rec_off: torch.Tensor, nslots: int, cap: i
         out = SegmentStats.empty(nstreams * nslots, dev)
     soa = out.soa()
     N.call("nvrx_records_stats", recs.data_ptr(), rec_off.data_ptr(), nstreams, nslots, cap, mode,
-           max_len, seg_off.data_ptr(), seg_len.data_ptr(), out_ns.data_ptr(), counts.data_ptr(),
+           max_len, seg_off.data_ptr(), seg_len.data_ptr(), out_ns.data_ptr(), N.ptr(counts),
            ctypes.byref(soa), N.ptr(col_ref), _stream(stream))
     return out
