@@ -45,6 +45,17 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 #ifndef NVRX_RB_ABLATE
 #define NVRX_RB_ABLATE 0
 #endif
+// Timing-only probes of an in-place reduction of the hot slots (outputs are
+// wrong): NVRX_RB_HOTPASS = k adds k passes over the register head and the LDS stash after the
+// scan, each record of local slot < 32 adding one non-returning LDS atomic into a 32 x 256-bin
+// histogram (a radix-select level); NVRX_RB_HOTP1 = 1 adds ds_min / ds_max per hot record to
+// pass 1 (the slot's MIN / MAX).  Both use the cold-bucket stage as scratch.
+#ifndef NVRX_RB_HOTPASS
+#define NVRX_RB_HOTPASS 0
+#endif
+#ifndef NVRX_RB_HOTP1
+#define NVRX_RB_HOTP1 0
+#endif
 
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
 // Slots one bucketing pass counts in LDS; a larger slot table is bucketed in passes over
@@ -180,6 +191,10 @@ void records_bucket_kernel(
             sink += ls;
         else if (ls < (uint32_t)nslots)
             atomicAdd(&cnt[ls], 1u);
+        if (NVRX_RB_HOTP1 && ls < 32u && stage_cap >= 8192) {
+            atomicMin(&stage[2 * ls], r.ns);
+            atomicMax(&stage[2 * ls + 1], r.ns);
+        }
     };
     if (RB_REGS > 0) {  // issued first: their latency overlaps the LDS-stashed head
 #pragma unroll
@@ -343,6 +358,26 @@ void records_bucket_kernel(
             place(nvrx_record{w.z, w.w});
         }
     };
+    if (NVRX_RB_HOTPASS > 0 && stage_cap >= 8192) {
+        for (int lvl = 0; lvl < NVRX_RB_HOTPASS; ++lvl) {
+            const uint32_t sh = 24u - 8u * (uint32_t)lvl;
+            const auto hp = [&](uint32_t slot, uint32_t ns) {
+                const uint32_t ls = slot - slot_lo;
+                if (ls < 32u) atomicAdd(&stage[ls * 256u + ((ns >> sh) & 255u)], 1u);
+            };
+#pragma unroll
+            for (int u = 0; u < RB_REGS; ++u) {
+                hp(reg[u].x, reg[u].y);
+                hp(reg[u].z, reg[u].w);
+            }
+            for (int64_t k = lane; k < snp; k += 64) {
+                const u32x4 w = wstash[k];
+                hp(w.x, w.y);
+                hp(w.z, w.w);
+            }
+            __syncthreads();
+        }
+    }
     if (RB_REGS > 0) {  // no memory dependency: their atomics and stores go out first
 #pragma unroll
         for (int u = 0; u < RB_REGS; ++u) {
