@@ -18,7 +18,10 @@ constexpr int CLS_MAX_BLOCKS = 1024;
 // segment lengths loaded per thread before any is classified: a block's chunk is tens of
 // thousands of segments, and one dependent load per 1024 of them left both passes
 // latency-bound (configs[3]: 153 + 118 us for 33.5 M segments)
-constexpr int CLS_BATCH = 8;
+#ifndef NVRX_CLS_BATCH  // build-time tuning constant
+#define NVRX_CLS_BATCH 8
+#endif
+constexpr int CLS_BATCH = NVRX_CLS_BATCH;
 
 
 // pass 1: per-block class counts (bcnt[b][c]); empty segments are written here

@@ -250,10 +250,22 @@ class MatrixReporter:
         on N GPUs (the partials exchange stays an eager collective)."""
         return ReportGraph(self, ns, s_push)
 
+    def graph_records(self, recs: torch.Tensor, rec_off: torch.Tensor) -> "ReportGraph":
+        """graph() over record streams resident in HBM (compute_stats_records captured)."""
+        return ReportGraph(self, None, 0, stats=lambda: self.compute_stats_records(recs, rec_off))
+
     def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False) -> "PipelinedReports":
         """Reports replayed two deep (1 GPU): report i+1's device work is queued before report
         i's results are read on the host, each report landing in its own pinned buffer."""
         return PipelinedReports(self, ns, s_push, timing)
+
+    def pipelined_records(self, recs: torch.Tensor, rec_off: torch.Tensor,
+                          timing: bool = False) -> "PipelinedReports":
+        """pipelined() over record streams resident in HBM (compute_stats_records: bucketing,
+        classification and the class kernels -- side-stream fork / join and stream-ordered
+        scratch included -- captured into the report graphs)."""
+        return PipelinedReports(self, None, 0, timing,
+                                stats=lambda: self.compute_stats_records(recs, rec_off))
 
     def _unpack(self, buf: Optional[torch.Tensor] = None) -> BatchResult:
         R = self.R
@@ -274,12 +286,14 @@ class ReportGraph:
     ~12 us per configs[1] report on MI355X (0.685 -> 0.673 ms, tools/ab_report_overhead.py).
     N GPUs: ``stats`` only; the partials exchange stays an eager collective."""
 
-    def __init__(self, rep: MatrixReporter, ns: torch.Tensor, s_push: int):
+    def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int, stats=None):
         self.rep = rep
-        _warm_up(rep, ns, s_push)
+        if stats is None:  # the statistics phase (record streams: MatrixReporter.graph_records)
+            stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
+        _warm_up(rep, stats)
         self.stats = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.stats):
-            rep.compute_stats(ns, s_push)
+            stats()
         self.rest = self.full = None
         if rep.exchange:
             # N GPUs: the shard's partials and the combine (+ the result copy) as graphs too;
@@ -298,7 +312,7 @@ class ReportGraph:
                 rep.h_out.copy_(rep.out, non_blocking=True)
             self.full = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.full):
-                rep.compute_stats(ns, s_push)
+                stats()
                 rep.compute_scores()
                 rep.h_out.copy_(rep.out, non_blocking=True)
 
@@ -326,16 +340,17 @@ class ReportGraph:
         return self.rep._unpack()
 
 
-def _warm_up(rep: MatrixReporter, ns: torch.Tensor, s_push: int) -> None:
-    """One eager report on a side stream (first-launch setup outside any graph capture).  The
-    individual history is restored afterwards: the warm-up must not fold whatever `ns` holds
-    now into it (the graphs' reports advance it exactly as report() does)."""
+def _warm_up(rep: MatrixReporter, stats) -> None:
+    """One eager report on a side stream (first-launch setup outside any graph capture);
+    stats() runs the statistics phase.  The individual history is restored afterwards: the
+    warm-up must not fold whatever the inputs hold now into it (the graphs' reports advance it
+    exactly as report() does)."""
     d = rep.device
     saved = rep.hist.clone() if rep.hist is not None else None
     side = torch.cuda.Stream(d)
     side.wait_stream(torch.cuda.current_stream(d))
     with torch.cuda.stream(side):
-        rep.compute_stats(ns, s_push)
+        stats()
         if not rep.exchange:
             rep.compute_scores()
         elif rep._fuse_ref():  # N GPUs: leave col_ref initialised without the exchange
@@ -365,20 +380,25 @@ class PipelinedReports:
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
-    statistics kernel on an otherwise idle device, for a sample of the reports."""
+    statistics kernel on an otherwise idle device, for a sample of the reports.
+    stats: the statistics phase as a callable (default: compute_stats(ns, s_push); record
+    streams: MatrixReporter.pipelined_records)."""
 
-    def __init__(self, rep: MatrixReporter, ns: torch.Tensor, s_push: int, timing: bool = False):
+    def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int,
+                 timing: bool = False, stats=None):
         if rep.exchange:
             raise RuntimeError("pipelined reports: 1 GPU (the partials exchange is an eager collective)")
         self.rep, self.timing = rep, timing
-        _warm_up(rep, ns, s_push)
+        if stats is None:
+            stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
+        _warm_up(rep, stats)
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
 
-        def capture(stats: bool, rest: bool, k: int):
+        def capture(with_stats: bool, rest: bool, k: int):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                if stats:
-                    rep.compute_stats(ns, s_push)
+                if with_stats:
+                    stats()
                 if rest:
                     # the scores kernel writes the pinned buffer itself when its epilogue stores
                     # the error word (fused reference, R <= FUSED_REF_MAX_ROWS); otherwise the

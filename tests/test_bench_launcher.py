@@ -71,7 +71,9 @@ def test_launcher_four_ranks_gloo_rehearsal():
     # GPU reports (f64 combine order aside)
     want = "hip_graph: statistics | score partials | eager all_gather | combine"
     assert cfg["launch_per_rank"] == [want] * 4 and lat["launch_per_rank"] == [want] * 4
+    assert zipf["launch_per_rank"] == [want] * 4
     one = _run(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
+    assert one["zipf_16384_ranks"]["launch_per_rank"] == ["hip_graph: whole reports, two in flight"]
     for leg in ("latency_4096_ranks", "zipf_16384_ranks"):
         a, b = line[leg]["scores"], one[leg]["scores"]
         assert a["stragglers_rel"] == b["stragglers_rel"], leg

@@ -93,3 +93,40 @@ def test_error_flags_per_report_and_column_reference_reset(R):
         pipe.submit()
         res, _ = pipe.collect()
         assert (res.err & 1) == want
+
+
+@pytest.mark.parametrize("R", [64, 300])
+def test_pipelined_records_matches_eager_reports(R):
+    """MatrixReporter.pipelined_records: record-stream reports (bucketing, classification, the
+    class kernels on the caller's and the side stream, stream-ordered scratch) captured as whole
+    graphs, two in flight -- report for report the results of eager report_records, the
+    individual history included.  R = 64 takes the fused reference and the pinned-buffer scores
+    epilogue, R = 300 the column reduction and the result copy."""
+    K, cap = 256, 128
+    counts = synth.zipf_counts(K, top=512)
+    slot, occ = synth.zipf_order(counts)
+    t = lambda a: torch.from_numpy(a.view(np.int32)).cuda()  # noqa: E731
+    N = slot.size
+    streams = [synth.synth_records(R, t(slot), t(occ), K, int(counts.max()), seed=11 + i)
+               for i in range(2)]
+    rec_off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * N
+    a = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    b = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
+    want = [a.report_records(streams[i % 2], rec_off) for i in range(5)]
+    recs = torch.empty_like(streams[0])
+    pipe = b.pipelined_records(recs, rec_off, timing=True)
+    got = []
+    for i in range(5):
+        recs.copy_(streams[i % 2])
+        pipe.submit(timed=i == 2)
+        res, ms = pipe.collect()
+        assert (ms is not None and ms > 0.0) if i == 2 else ms is None
+        got.append(res)
+    for w, g in zip(want, got):
+        assert g.err == w.err == 0
+        np.testing.assert_array_equal(w.gpu_relative, g.gpu_relative)
+        np.testing.assert_array_equal(w.gpu_individual, g.gpu_individual)
+        np.testing.assert_array_equal(w.stragglers_relative, g.stragglers_relative)
+        np.testing.assert_array_equal(w.stragglers_individual, g.stragglers_individual)
+    for f in ("num", "min", "max", "med", "avg", "std"):
+        assert torch.equal(getattr(a.stats, f).view(torch.int32), getattr(b.stats, f).view(torch.int32)), f
