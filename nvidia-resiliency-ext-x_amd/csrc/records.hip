@@ -56,18 +56,6 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 #ifndef NVRX_RB_HOTP1
 #define NVRX_RB_HOTP1 0
 #endif
-// NVRX_RB_PF_KB > 0 (build-time tuning constant): once pass 2 has placed the register-held head
-// (its registers free again), the block touches one dword per NVRX_RB_PF_LINE bytes of the first
-// NVRX_RB_PF_KB KiB of stream t + pf_ahead -- the stream a CU is likely to start about one block
-// later -- so that stream's pass 1 finds its lines in the Infinity Cache instead of HBM.  (LDS-DMA
-// loads into a dump region would need no registers, but the compiler then waits for them before
-// every LDS access of pass 2.)
-#ifndef NVRX_RB_PF_KB
-#define NVRX_RB_PF_KB 0
-#endif
-#ifndef NVRX_RB_PF_LINE
-#define NVRX_RB_PF_LINE 64
-#endif
 
 constexpr uint32_t RB_OVF = 0x80000000u;  // start[s] flag: slot s overflowed its ring
 // Slots one bucketing pass counts in LDS; a larger slot table is bucketed in passes over
@@ -144,7 +132,7 @@ void records_bucket_kernel(
     int64_t cap, int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
     int32_t* counts, int64_t stash_pairs, int64_t stage_cap, uint32_t cold_max,
     nvrx_stats_soa tiny, uint32_t slot_lo, int64_t seg_stride, int pass, int64_t t0,
-    int64_t nstreams_total, int64_t pf_ahead) {
+    int64_t nstreams_total) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* cnt = lds;                // [nslots] pushes per slot
     uint32_t* cur = lds + nslots;       // [nslots] scatter cursor / occurrence counter
@@ -397,21 +385,6 @@ void records_bucket_kernel(
             place(nvrx_record{reg[u].z, reg[u].w});
         }
     }
-    constexpr int PF_N = NVRX_RB_PF_KB > 0 ? (NVRX_RB_PF_KB * 1024 / NVRX_RB_PF_LINE + 64 * RB_WAVES - 1) / (64 * RB_WAVES) : 1;
-    uint32_t pf[PF_N];
-    if (NVRX_RB_PF_KB > 0) {
-        // (indexed from the kernel argument, so the loads stay global, not flat: a flat load
-        // also counts in lgkmcnt, which pass 2's LDS atomics wait on)
-        const int64_t tn = t + pf_ahead;
-        const uint32_t* w = (const uint32_t*)recs;  // 2 words per record
-        const int64_t w0 = tn < nstreams_total ? 2 * rec_off[tn] : 0;
-        const int64_t w1 = tn < nstreams_total ? min(2 * rec_off[tn + 1], w0 + NVRX_RB_PF_KB * 256) : 0;
-#pragma unroll
-        for (int k = 0; k < PF_N; ++k) {
-            const int64_t i = w0 + ((int64_t)k * blockDim.x + threadIdx.x) * (NVRX_RB_PF_LINE / 4);
-            pf[k] = i < w1 ? w[i] : 0u;
-        }
-    }
     {
         const int64_t iters = (np - held) / (64 * RB_UNROLL);
         const int per_it = iters > 0 ? (int)((snp / 64 + iters - 1) / iters) : 0;
@@ -435,12 +408,6 @@ void records_bucket_kernel(
         place_stash(1 << 30);
         // a chunk that is not pair-aligned (np = 0): its records one by one
         if (!wpairs) for_records(rs, lo, hi, lane, false, place);
-    }
-    if (NVRX_RB_PF_KB > 0) {  // the touched lines have landed (nothing reads them here)
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < PF_N; ++k) x ^= pf[k];
-        asm volatile("" ::"v"(x));
     }
     if (NVRX_RB_ABLATE == 2) return;
     if (stage_lim > 0) {  // the assembled head of the bucket array, in 16-byte stores
@@ -541,18 +508,6 @@ constexpr int RB_COLD = 512;     // largest cold bucket (records)
 constexpr int RB_WAVES = NVRX_RB_WAVES;
 constexpr int RB_REGS = RB_REGS_PER_BLOCK / (64 * RB_WAVES);
 
-static int64_t rb_cu_count() {  // streams resident at once: one block per CU
-    static int64_t n = 0;
-    if (n == 0) {
-        int dev = 0, c = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-            c = 256;
-        n = c;
-    }
-    return n;
-}
-
 static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* rec_off, int64_t t0,
                                       int64_t nlaunch, int64_t nstreams, int64_t nslots, int64_t cap,
                                       int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
@@ -594,7 +549,7 @@ static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* re
     hipLaunchKernelGGL((records_bucket_kernel<RB_WAVES, RB_REGS>), dim3((unsigned)nlaunch), dim3(64 * RB_WAVES),
                        lds_launch, st, recs, rec_off, nslots, cap, force_stable, seg_off, seg_len, out_ns,
                        counts, stash_pairs, stage_cap, (uint32_t)RB_COLD, tiny_soa, slot_lo, seg_stride, pass,
-                       t0, nstreams, rb_cu_count());
+                       t0, nstreams);
     return hipGetLastError();
 }
 
