@@ -61,6 +61,14 @@ fz = batch.MatrixReporter(Rz, Kz, cap=8192, thr_rel=0.8, exchange=False).report_
 xz = batch.MatrixReporter(Rz, Kz, cap=8192, thr_rel=0.8, exchange=True).report_records(recs, off)
 errs.append(maxrel(xz.gpu_relative, fz.gpu_relative))
 sets.append(same(fz, xz))
+# ... and as the N-GPU bench leg runs it: statistics, partials and combine as graphs, the
+# all_gather eager (MatrixReporter.graph_records)
+gz = batch.MatrixReporter(Rz, Kz, cap=8192, thr_rel=0.8, exchange=True).graph_records(recs, off)
+for _ in range(2):
+    gz.run_stats()
+    yz = gz.run_rest()
+    errs.append(maxrel(yz.gpu_relative, fz.gpu_relative))
+    sets.append(same(fz, yz))
 out.update(errs=errs, sets=sets, nrel=int(xz.stragglers_relative.sum()))
 torch.distributed.destroy_process_group()
 print("RESULT " + json.dumps(out))
