@@ -228,7 +228,8 @@ int nvrx_records_bucket(const nvrx_record* recs, const int64_t* rec_off, int64_t
  * (host-known); col_ref (optional, [2*nslots]) as for nvrx_segment_stats_strided (rows =
  * streams), produced by a column reduction; counts may be NULL here (the pushes per bucket are
  * then not written: 4 B per (stream, slot) less).  On return seg_len[g] < 0 marks a bucket of
- * -seg_len[g] records whose statistics the bucketing kernel computed itself. */
+ * -seg_len[g] records whose statistics the bucketing kernel computed itself; neither its
+ * seg_off[g] nor its records in out_ns are written. */
 int nvrx_records_stats(const nvrx_record* recs, const int64_t* rec_off, int64_t nstreams,
                        int64_t nslots, int64_t cap, int32_t mode, int64_t max_len, int64_t* seg_off,
                        int32_t* seg_len, uint32_t* out_ns, int32_t* counts,

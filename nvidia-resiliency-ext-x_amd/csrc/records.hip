@@ -50,6 +50,9 @@ __device__ __forceinline__ int64_t stream_base(const int64_t* rec_off, int64_t t
 // scan, each record of local slot < 32 adding one non-returning LDS atomic into a 32 x 256-bin
 // histogram (a radix-select level); NVRX_RB_HOTP1 = 1 adds ds_min / ds_max per hot record to
 // pass 1 (the slot's MIN / MAX).  Both use the cold-bucket stage as scratch.
+#ifndef NVRX_RB_TINY_COPY  // build-time switch: 1 = also write the reduced tiny buckets (and offsets) out
+#define NVRX_RB_TINY_COPY 0
+#endif
 #ifndef NVRX_RB_HOTPASS
 #define NVRX_RB_HOTPASS 0
 #endif
@@ -266,7 +269,7 @@ void records_bucket_kernel(
         if (threadIdx.x == 0 && wtot[0][0] == 0x12345u) counts[0] = 1;
         return;
     }
-    uint32_t cold_total = 0;
+    uint32_t cold_total = 0, tiny_end = 0;
     {
         // the tier totals and this wave's carries from the waves' chunk totals: lane w reads
         // wave w's, one wave reduction each (a serial walk over the waves' totals, 16 dependent
@@ -275,6 +278,7 @@ void records_bucket_kernel(
         const uint32_t w1 = lane < RB_WAVES ? wtot[1][lane] : 0u;
         const uint32_t w2 = lane < RB_WAVES ? wtot[2][lane] : 0u;
         const uint32_t tiny_total = wave_sum_u32(w0);
+        tiny_end = tiny_total;
         cold_total = tiny_total + wave_sum_u32(w1);
         const uint32_t lim = (uint32_t)min((int64_t)cold_total, stage_cap);
         bool overflow = false;
@@ -311,7 +315,8 @@ void records_bucket_kernel(
                     // a bucket this kernel reduces itself (after pass 2): a negative length
                     const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
                     if (NVRX_RB_ABLATE != 7) {  // 7: the scans without their global stores
-                        seg_off[g] = ns_off + base + st;
+                        // a reduced bucket's offset is never read (records_stats: not written)
+                        if (!reduced || NVRX_RB_TINY_COPY) seg_off[g] = ns_off + base + st;
                         seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
                         if (counts) counts[g] = (int32_t)total;  // optional in records_stats
                     }
@@ -414,7 +419,11 @@ void records_bucket_kernel(
         __syncthreads();
         const u32x4* sv = (const u32x4*)stage;
         u32x4* ov = (u32x4*)out;  // out = stream base: 16-byte aligned
-        for (uint32_t i = threadIdx.x; i < stage_lim / 4; i += blockDim.x) ov[i] = sv[i];
+        // records_stats with the whole tiny tier staged: every tiny bucket is reduced below from
+        // LDS and flagged (negative seg_len), so its records are never read from out_ns -- the
+        // copy-out starts past them (NVRX_RB_TINY_COPY=1 writes them anyway)
+        const uint32_t skip = (tiny.num && !NVRX_RB_TINY_COPY && tiny_end <= stage_lim) ? tiny_end / 4 : 0u;
+        for (uint32_t i = skip + threadIdx.x; i < stage_lim / 4; i += blockDim.x) ov[i] = sv[i];
         // records_stats: the statistics of the staged buckets of <= RB_TINY records, one lane
         // per bucket straight from LDS (lane_stats: computeStats bit for bit, as the ragged
         // lane<8> class does), instead of a later kernel re-reading them through a class list
