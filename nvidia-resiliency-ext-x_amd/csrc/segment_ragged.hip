@@ -28,7 +28,10 @@ using namespace ragged;
 
 // The class kernels are dealt over the caller's stream and one side stream per device
 // (configs[3]: 4.28 -> 4.15 ms; 3 / 4 streams were no faster).
-constexpr int RAGGED_STREAMS = 2;
+#ifndef NVRX_RAGGED_STREAMS  // build-time tuning constant
+#define NVRX_RAGGED_STREAMS 2
+#endif
+constexpr int RAGGED_STREAMS = NVRX_RAGGED_STREAMS;
 struct Fork {
     hipStream_t s[RAGGED_STREAMS];  // s[0] unused: slot 0 is the caller's stream
     hipEvent_t fork, join[RAGGED_STREAMS];
