@@ -505,7 +505,10 @@ constexpr int RB_REGS_PER_BLOCK = NVRX_RB_REGS_PER_BLOCK;
 #define NVRX_RB_STAGE_KB 96
 #endif
 constexpr int RB_STAGE_KB = NVRX_RB_STAGE_KB;  // LDS staging of the cold buckets
-constexpr int RB_COLD = 512;     // largest cold bucket (records)
+#ifndef NVRX_RB_COLD  // build-time tuning constant
+#define NVRX_RB_COLD 512
+#endif
+constexpr int RB_COLD = NVRX_RB_COLD;  // largest cold bucket (records)
 
 // The shipped configuration: 16 waves x 16 register pairs per lane (4 waves / SIMD, 128
 // VGPRs), LDS stash interleaved with pass 2, 96 KiB of cold-bucket staging, cold = keep <= 512.
