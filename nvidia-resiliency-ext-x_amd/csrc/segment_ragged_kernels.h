@@ -22,6 +22,7 @@ constexpr int CLS_MAX_BLOCKS = 1024;
 #define NVRX_CLS_BATCH 8
 #endif
 constexpr int CLS_BATCH = NVRX_CLS_BATCH;
+static_assert(CLS_BATCH >= 1 && CLS_BATCH < 32 && 5 * NCLASS <= 64, "5-bit packed class counts per batch");
 
 
 // pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
@@ -46,6 +47,9 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
             const int64_t s = b + j * CLS_THREADS + threadIdx.x;
             n[j] = s < hi ? segs.kept_len(s) : -1;
         }
+        // the batch's class counts packed 5 bits per class in one 64-bit word (one shift and
+        // add per segment instead of a compare and add per class), unpacked once per batch
+        uint64_t pk = 0;
 #pragma unroll
         for (int j = 0; j < CLS_BATCH; ++j) {
             const int64_t s = b + j * CLS_THREADS + threadIdx.x;
@@ -53,11 +57,11 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
                 write_empty(out, s);
                 cr.miss(s);
             } else if (n[j] > 0) {  // n < 0: reduced elsewhere (or past the chunk)
-                const int cls = seg_class(n[j], aligned16 != 0, exact != 0);
-#pragma unroll
-                for (int c = 0; c < NCLASS; ++c) mine[c] += cls == c ? 1u : 0u;
+                pk += 1ull << (5 * seg_class(n[j], aligned16 != 0, exact != 0));
             }
         }
+#pragma unroll
+        for (int c = 0; c < NCLASS; ++c) mine[c] += (uint32_t)(pk >> (5 * c)) & 31u;
     }
 #pragma unroll
     for (int c = 0; c < NCLASS; ++c) {
