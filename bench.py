@@ -115,6 +115,20 @@ def make_shard(R, K_global, s_push, world, rank, dev):
 
 
 TIMED_REPORTS = 10  # statistics-kernel timing phase after the throughput loop
+# Untimed warm-up runs at least `warmup` reports AND at least this long: MI355X clocks ramp under
+# sustained load, and a timed run that starts after a few milliseconds of work reads ~3 % slower
+# per report at 20 reports (tools/probe_pipeline_fill.py, profiles/r04/pipeline_fill.json)
+WARMUP_MIN_MS = 40.0
+
+
+def warm(step, n_min: int, world: int) -> int:
+    """step() at least n_min times and, on one rank, until WARMUP_MIN_MS elapsed (on N ranks a
+    step may hold a collective, so every rank runs the same count: n_min); returns the count."""
+    t0, n = time.perf_counter(), 0
+    while n < n_min or (world == 1 and (time.perf_counter() - t0) * 1e3 < WARMUP_MIN_MS):
+        step()
+        n += 1
+    return n
 
 
 def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True):
@@ -134,9 +148,10 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         # unpack of the results the scores kernel wrote to pinned memory) inside the timed
         # region, which holds nothing but back-to-back reports
         pipe = rep.pipelined(ns, s_push, timing=time_kernel)
-        for _ in range(max(1, warmup)):
+        def one():
             pipe.submit()
-            res, _ = pipe.collect()
+            pipe.collect()
+        warm(one, max(1, warmup), world)
         barrier(world)
         t0 = time.perf_counter()
         pipe.submit()
@@ -164,8 +179,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
     # only the all_gather of the partials between them is an eager collective
     g = rep.graph(ns, s_push) if use_graph else None
     if g is not None:
-        for _ in range(max(1, warmup)):
-            res = g.run()
+        warm(g.run, max(1, warmup), world)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     barrier(world)
@@ -231,9 +245,10 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
         # 1 GPU: whole-report graphs two in flight, as the headline (MatrixReporter.
         # pipelined_records); the statistics phase timed afterwards on an idle device
         pipe = rep.pipelined_records(recs, rec_off, timing=True)
-        for _ in range(max(1, warmup)):
+        def one():
             pipe.submit()
-            res, _ = pipe.collect()
+            pipe.collect()
+        warm(one, max(1, warmup), world)
         barrier(world)
         t0 = time.perf_counter()
         pipe.submit()
@@ -253,8 +268,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
         # N GPUs: as the other legs -- statistics, score partials and combine as HIP graphs,
         # the all_gather of the partials eager between them
         g = rep.graph_records(recs, rec_off)
-        for _ in range(max(1, warmup)):
-            res = g.run()
+        warm(g.run, max(1, warmup), world)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
         barrier(world)
@@ -523,7 +537,7 @@ def main():
             "unit": "samples/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": args.warmup, "warmup_min_ms": WARMUP_MIN_MS,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",

@@ -25,8 +25,16 @@ for _ in range(5):
     pipe.submit()
     pipe.collect()
 out = {}
-for idle_ms in (0, 50):
-    for steps in (20, 100):
+for idle_ms, steps in ((0, 20), (0, 100), (50, 20), (50, 100), (-1, 20), (0, 20)):
+    if idle_ms < 0:  # a long busy period right before: 150 reports, then the 20 timed
+        for _ in range(150):
+            pipe.submit()
+            pipe.collect()
+        idle_ms = 0
+        tag = "hot"
+    else:
+        tag = ""
+    if True:
         torch.cuda.synchronize()
         time.sleep(idle_ms / 1e3)
         t0 = time.perf_counter()
@@ -40,7 +48,21 @@ for idle_ms in (0, 50):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         d = np.diff([0.0] + land) * 1e3
-        out[f"idle{idle_ms}_n{steps}"] = dict(ms_per_report=el / steps * 1e3, first=float(d[0]),
+        out[f"{tag}idle{idle_ms}_n{steps}" + ("_again" if f"{tag}idle{idle_ms}_n{steps}" in out else "")] = dict(ms_per_report=el / steps * 1e3, first=float(d[0]),
                                               second=float(d[1]), median=float(np.median(d[2:])),
                                               last=float(d[-1]))
+# host cost of the calls themselves (20-report burst): submit() = graph replay + event record
+torch.cuda.synchronize()
+sub, col = [], []
+t0 = time.perf_counter()
+a = time.perf_counter(); pipe.submit(); sub.append(time.perf_counter() - a)
+for i in range(20):
+    if i + 1 < 20:
+        a = time.perf_counter(); pipe.submit(); sub.append(time.perf_counter() - a)
+    a = time.perf_counter(); pipe.collect(); col.append(time.perf_counter() - a)
+torch.cuda.synchronize()
+out["host_us"] = dict(submit=[round(x * 1e6, 1) for x in sub[:4]], submit_median=float(np.median(sub) * 1e6),
+                      collect=[round(x * 1e6, 1) for x in col[:4]], collect_median=float(np.median(col) * 1e6))
+g = pipe.full[0]
+out["raw_graph_exec"] = hasattr(g, "raw_cuda_graph_exec")
 print(json.dumps(out, indent=1))
