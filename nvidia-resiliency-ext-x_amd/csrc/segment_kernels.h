@@ -234,12 +234,15 @@ __device__ __forceinline__ void wide_moments(const uint32_t* p, int n, int64_t s
     }
 }
 
+#ifndef NVRX_BINS_PER_SAMPLE_SHORT  // build-time tuning constant: bins per lane-sample, PL <= 8
+#define NVRX_BINS_PER_SAMPLE_SHORT 16
+#endif
 template <int PL>
 struct Bins {
     // bins per wave: 16 per lane-sample for short segments (PL <= 16: C3's 1024 samples take
     // 256 bins -- fewer bucket-mates of the median to compact and rank, 3-5 % faster than 128,
     // while 512 was slower), 8 above (PL = 32 was fastest at 256)
-    static constexpr int PB = PL <= 16 ? 16 * PL : 8 * PL;
+    static constexpr int PB = PL <= 8 ? NVRX_BINS_PER_SAMPLE_SHORT * PL : PL <= 16 ? 16 * PL : 8 * PL;
     static constexpr int NB = PB < 64 ? 64 : PB > 512 ? 512 : PB;
     static constexpr int BPL = NB / 64;                     // bins per lane
     static constexpr int LOG = (NB == 64) ? 6 : (NB == 128) ? 7 : (NB == 256) ? 8 : (NB == 512) ? 9 : 10;
