@@ -216,9 +216,15 @@ template <int PL>
 struct ListGroup {  // one epilogue per chunk (emit_lane): the short classes, whose chunks are long
     static constexpr bool on = PL <= 8;
 };
+#ifndef NVRX_LIST4_OCC  // build-time tuning constants: waves per SIMD of list<4> / list<8>
+#define NVRX_LIST4_OCC 8
+#endif
+#ifndef NVRX_LIST8_OCC
+#define NVRX_LIST8_OCC 7
+#endif
 template <int PL>
 struct ListOcc {  // the prefetch buffer costs PL more VGPRs, the chunk's results nine
-    static constexpr int W = PL == 16 ? 6 : PL == 8 ? 7 : OccV<PL, false>::W;
+    static constexpr int W = PL == 16 ? 6 : PL == 8 ? NVRX_LIST8_OCC : PL == 4 ? NVRX_LIST4_OCC : OccV<PL, false>::W;
 };
 #ifndef NVRX_LIST_CHUNK  // build-time tuning constant (tools/build_variant.sh)
 #define NVRX_LIST_CHUNK 16
