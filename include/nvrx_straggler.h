@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NVRX_ABI_VERSION 4
+#define NVRX_ABI_VERSION 5
 
 #define NVRX_OK 0
 #define NVRX_ERR_INVALID -1   /* bad argument / shape */
@@ -333,6 +333,16 @@ typedef struct nvrx_capture_counters {
      * first buffer callback it delivered, the callbacks delivered during flushes, and the time
      * from a flush's last callback to its return */
     int64_t flush_first_cb_ns, flush_callbacks, flush_tail_ns;
+    /* flush completeness (capture.cpp, top): job dispatches counted at enqueue (the external
+     * correlation id request), flushes that waited for every counted dispatch enqueued before
+     * them, flushes without that count (marking off: NVRX_CAPTURE_MARKING=0 or the service
+     * refused; a 200 us quiet period / the ENQUEUE count / the buffer flush alone), counted
+     * flushes that timed out (NVRX_CAPTURE_FLUSH_TIMEOUT_MS, default 1000: a kernel still running)
+     * and the dispatches they gave up on (delivered to a later report).  delivery: 0 buffer,
+     * 1 callback (default), 2 callback_counted, -1 capture not configured; marking: 1 when the
+     * request service is on. */
+    int64_t enqueues_counted, counted_flushes, quiet_flushes, flush_timeouts, owed_abandoned;
+    int32_t delivery, marking;
 } nvrx_capture_counters;
 int nvrx_capture_stats(nvrx_capture_counters* out);
 

@@ -6,12 +6,28 @@
 // kernel name, block dims, grid dims in blocks) and pushes (end - start) / 1000.0f into that
 // key's ring.  Here a rocprofiler-sdk tool owns two contexts:
 //   * "symbols"  (started at configuration): code-object callback tracing, kernel_id -> name;
-//   * "dispatch" (started / stopped with the profiler handle): buffer tracing of
-//     ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH.
-// The buffer callback turns each completed dispatch into the reference's key (workgroup
-// size = block dims; grid_size is in work-items, so blocks = grid_size / workgroup_size) and
-// an integer-ns duration record appended to the profiler handle's record log; the per-key
-// rings and statistics are then the HIP kernels of the report path.
+//   * "dispatch" (started / stopped with the profiler handle): KERNEL_DISPATCH callback tracing
+//     (the default; NVRX_CAPTURE_DELIVERY=buffer selects buffer tracing instead), plus the
+//     external-correlation-id request service that marks the library's own report kernels and
+//     counts every job dispatch at enqueue (below).
+// Each completed dispatch becomes the reference's key (workgroup size = block dims; grid_size is
+// in work-items, so blocks = ceil(grid_size / workgroup_size)) and an integer-ns duration record
+// queued for the profiler handle; the per-key rings and statistics are then the HIP kernels of
+// the report path.
+//
+// Flush completeness.  The reference's getStats calls cuptiActivityFlushAll(0) after the
+// Detector's torch.cuda.synchronize() (CuptiProfiler.cpp:138, straggler.py:234-235): every kernel
+// that completed is in the report.  rocprofiler-sdk hands a completion over on the runtime's
+// signal-handler thread, some time after the device finished -- long after it when the host is
+// loaded.  So every job dispatch is counted at enqueue, in the external-correlation-id request
+// rocprofiler-sdk makes on the launching thread (a callback that is on anyway for the marking, so
+// the count is one atomic add), under the current flush EPOCH, which the request hands back as
+// the dispatch's external correlation id.  Its completion subtracts it from that epoch once the
+// record is queued.  A flush opens a new epoch and waits until no earlier epoch is owed anything:
+// every dispatch enqueued before the flush has then been handed over, however late the runtime's
+// thread ran.  A dispatch that is still running (enqueued by another thread after the caller's
+// synchronize) is waited for up to NVRX_CAPTURE_FLUSH_TIMEOUT_MS (default 1000); then its epoch
+// is given up, counted (flush_timeouts, owed_abandoned), and the record joins a later report.
 //
 // rocprofiler-sdk tools configure when the ROCm runtime initialises: nvrx_capture_configure
 // must run before the process's first HIP call (the Python side does it at
@@ -36,6 +52,9 @@
 
 namespace {
 
+constexpr int kEpochs = 1024;  // epoch slots: a slot is reused kEpochs flushes later
+constexpr int kMarks = 16;     // threads that may run a report of their own at once
+
 struct Capture {
     std::mutex mu;
     std::unordered_map<uint64_t, std::string> names;  // kernel_id -> kernel name
@@ -45,24 +64,20 @@ struct Capture {
     std::atomic<bool> ready{false};      // tool_init completed
     std::atomic<bool> requested{false};  // nvrx_capture_configure succeeded
     std::atomic<nvrx_profiler*> target{nullptr};
-    std::atomic<int> inflight{0};        // buffer callbacks running (destroy waits for 0)
+    std::atomic<int> inflight{0};        // delivery callbacks running (detach waits for 0)
     // cost accounting (nvrx_capture_stats): callbacks, headers, dispatch records handed to the
-    // profiler, time inside our callback, flushes and time inside rocprofiler_flush_buffer
+    // profiler, time inside our callback, flushes and their wall time
     std::atomic<uint64_t> n_cb{0}, n_rec{0}, n_pushed{0}, cb_ns{0}, n_flush{0}, flush_ns{0};
     // where a report-time flush's time goes: steady-clock ns of the flush in progress (0: none),
-    // and per flush the time to the first buffer callback it caused, the callbacks it caused,
-    // and the time from the end of its last callback to rocprofiler_flush_buffer's return
+    // and per flush the time to the first delivery callback it saw, the callbacks it saw, and
+    // the time from the end of its last callback to its return
     std::atomic<int64_t> flush_t0{0}, last_cb_end{0};
     std::atomic<uint64_t> flush_first_cb_ns{0}, flush_cbs{0}, flush_tail_ns{0};
-    // delivery (NVRX_CAPTURE_DELIVERY): 0 = buffer (records batched by rocprofiler-sdk, a report
-    // flushes the buffer: ~3.4-5 ms whenever records are pending, of which all but ~35 us come
-    // after our callback has returned -- rocprofiler-sdk's own wait), 1 = callback, the default
-    // (each completed dispatch handed over as its completion is processed; a flush waits for a
-    // 200 us quiet period), 2 = callback_counted (1 + the enqueues counted, so a flush waits for
-    // exactly those completions, ~1 us -- but the enqueue callbacks on the launching thread cost
-    // the training step more).  GPT-2 small, batch 8, profiling_interval 1, interleaved:
-    // step overhead 9.2 / 11.2 / 13.7 % (callback / buffer / counted, medians of 3), report-time
-    // flush 0.2 / 3.5 / 0.005 ms (profiles/r04/live_delivery.json, capture_delivery.json).
+    // delivery (NVRX_CAPTURE_DELIVERY): 0 = buffer (records batched by rocprofiler-sdk; a flush
+    // also flushes the buffer, ~3.4-5 ms whenever records are pending), 1 = callback, the
+    // default (each completed dispatch handed over as the runtime processes its completion),
+    // 2 = callback_counted (1 + ENQUEUE callbacks on the launching thread, which count the
+    // dispatches when the marking service below is off; kept for cost attribution).
     int delivery = 1;
     std::atomic<uint64_t> n_enqueued{0}, n_completed{0};
     // callback delivery runs on the runtime's completion (signal-handler) thread, which must never
@@ -74,11 +89,20 @@ struct Capture {
     std::vector<nvrx::DispatchRec> queue;
     std::atomic<uint64_t> n_runtime{0};  // runtime copy / fill dispatches left out (below)
     bool keep_runtime = false;           // NVRX_CAPTURE_RUNTIME_KERNELS=1 keeps them
-    // the library's own report kernels (get_stats / get_records / reset / ingest) are marked
-    // through an external correlation id set for the reporting thread only and left out
+    // the external-correlation-id request service (NVRX_CAPTURE_MARKING=0 turns it off, for cost
+    // attribution): marks the library's own report kernels (left out) and counts job dispatches
+    bool marking = false;
     std::atomic<uint64_t> n_own{0};
-    std::atomic<uint64_t> self_tid{0};  // rocprofiler thread id of the report in progress (0: none)
-    bool self_marking = false;          // the external correlation id request service is on
+    std::atomic<int> n_marked{0};                  // threads currently marked
+    std::atomic<uint64_t> marks[kMarks] = {};      // their rocprofiler thread ids (0: free)
+    // flush epochs (see the top of the file); only a flush advances `epoch`, under flush_mu
+    std::atomic<uint64_t> epoch{1};
+    std::atomic<int64_t> owed[kEpochs] = {};
+    std::mutex flush_mu;
+    uint64_t settled = 1;  // lowest epoch that may still be owed (flush_mu)
+    int64_t flush_timeout_ms = 1000;
+    std::atomic<uint64_t> n_requested{0}, n_counted_flush{0}, n_quiet_flush{0}, n_timeouts{0},
+        n_abandoned{0};
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -101,23 +125,49 @@ void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_us
     cap().names[d->kernel_id] = std::move(n);
 }
 
-// The reference's getStats runs on the host and adds no activity of its own; this library's
-// report runs HIP kernels.  They are told apart from the job's by thread: while a report is in
-// progress on thread T, rocprofiler-sdk's request for the external correlation id of a kernel
-// dispatch made on T gets SELF_MARK, and the buffer callback drops those records.  Kernels other
-// threads launch meanwhile keep being captured, as CUPTI keeps its activity enabled through
-// getStats (a pause of the whole dispatch context would lose them).
+// External correlation ids of the dispatch context.  The reference's getStats runs on the host and
+// adds no activity of its own; this library's report runs HIP kernels.  They are told apart from
+// the job's by thread: while a report is in progress on thread T (T in `marks`), the request for a
+// dispatch made on T gets SELF_MARK and the delivery drops that record.  Kernels other threads
+// launch meanwhile keep being captured, as CUPTI keeps its activity enabled through getStats (a
+// pause of the whole dispatch context would lose them).  Every other dispatch gets JOB_TAG | the
+// current flush epoch, and is counted as owed in that epoch.
 constexpr uint64_t SELF_MARK = 0x4E56525853454C46ull;  // "NVRXSELF"
+constexpr uint64_t JOB_TAG = 0x4A4F42ull << 40;          // "JOB" | 40-bit epoch
+constexpr uint64_t EPOCH_MASK = (1ull << 40) - 1;
+
+bool marked_thread(uint64_t tid) {
+    Capture& c = cap();
+    if (c.n_marked.load(std::memory_order_acquire) == 0) return false;
+    for (auto& m : c.marks)
+        if (m.load(std::memory_order_relaxed) == tid) return true;
+    return false;
+}
 
 int external_corr_request(rocprofiler_thread_id_t tid, rocprofiler_context_id_t,
                           rocprofiler_external_correlation_id_request_kind_t, rocprofiler_tracing_operation_t,
                           uint64_t, rocprofiler_user_data_t* value, void*) {
-    const uint64_t self = cap().self_tid.load(std::memory_order_acquire);
-    if (self != 0 && tid == self) {
+    Capture& c = cap();
+    if (tid != 0 && marked_thread(tid)) {
         value->value = SELF_MARK;
         return 0;
     }
-    return 1;  // no value of ours: the thread's pushed default (none)
+    const uint64_t e = c.epoch.load(std::memory_order_acquire);
+    c.owed[e % kEpochs].fetch_add(1, std::memory_order_relaxed);
+    c.n_requested.fetch_add(1, std::memory_order_relaxed);
+    value->value = JOB_TAG | e;
+    return 0;
+}
+
+// a delivered dispatch (job, runtime blit or, untagged, anything else) is no longer owed: called
+// after its record is queued / pushed, so a flush that sees its epoch settled also drains it
+void settle(uint64_t external) {
+    if ((external & ~EPOCH_MASK) != JOB_TAG) return;
+    Capture& c = cap();
+    const uint64_t e = external & EPOCH_MASK;
+    // an epoch given up long ago: its slot may already count a newer epoch
+    if (c.epoch.load(std::memory_order_relaxed) - e >= kEpochs / 2) return;
+    c.owed[e % kEpochs].fetch_sub(1, std::memory_order_release);
 }
 
 // The reference enables only CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL (CuptiProfiler.cpp:118) and
@@ -154,8 +204,8 @@ std::string composite_name(const nvrx::DispatchKey& k) {
     return std::string(buf.data());
 }
 
-// One completed dispatch -> the reference's record, or false when it is not the job's kernel
-// (a report kernel of ours, or a runtime blit).
+// One completed dispatch -> the reference's record, or not the job's kernel (a report kernel of
+// ours, or a runtime blit).
 enum class Kind { job, own, runtime };
 Kind to_dispatch(const rocprofiler_kernel_dispatch_info_t& di, uint64_t start, uint64_t end,
                  uint64_t external, nvrx::DispatchRec& d) {
@@ -204,9 +254,10 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
     CallbackScope scope;
     Capture& c = scope.c;
     nvrx_profiler* p = c.target.load();
-    if (!p) return;
     thread_local std::vector<nvrx::DispatchRec> batch;
+    thread_local std::vector<uint64_t> tags;
     batch.clear();
+    tags.clear();
     uint64_t runtime = 0, own = 0;
     for (size_t i = 0; i < num_headers; ++i) {
         const rocprofiler_record_header_t* h = headers[i];
@@ -214,6 +265,8 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
             h->kind != ROCPROFILER_BUFFER_TRACING_KERNEL_DISPATCH)
             continue;
         auto* r = static_cast<const rocprofiler_buffer_tracing_kernel_dispatch_record_t*>(h->payload);
+        tags.push_back(r->correlation_id.external.value);
+        if (!p) continue;
         nvrx::DispatchRec d;
         switch (to_dispatch(r->dispatch_info, r->start_timestamp, r->end_timestamp,
                             r->correlation_id.external.value, d)) {
@@ -228,13 +281,12 @@ void dispatch_buffer_cb(rocprofiler_context_id_t, rocprofiler_buffer_id_t,
     c.n_runtime.fetch_add(runtime);
     c.n_own.fetch_add(own);
     if (!batch.empty()) nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
+    for (uint64_t t : tags) settle(t);  // after the push: a settled epoch's records are in p
 }
 
-// callback delivery (NVRX_CAPTURE_DELIVERY=callback): rocprofiler-sdk's KERNEL_DISPATCH callback
-// tracing hands over each dispatch once the runtime has processed its completion signal -- no
-// buffer, so a report has nothing to flush but the completions still being processed.  With the
-// ENQUEUE operation too (=callback_counted) the enqueued dispatches are counted, and a flush
-// waits for exactly those completions.
+// callback delivery (NVRX_CAPTURE_DELIVERY=callback, the default): rocprofiler-sdk's
+// KERNEL_DISPATCH callback tracing hands over each dispatch once the runtime has processed its
+// completion signal -- no buffer to flush, only completions still being processed to wait for.
 void dispatch_callback_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_user_data_t*, void*) {
     Capture& c = cap();
     if (record.kind != ROCPROFILER_CALLBACK_TRACING_KERNEL_DISPATCH) return;
@@ -262,7 +314,20 @@ void dispatch_callback_cb(rocprofiler_callback_tracing_record_t record, rocprofi
             c.n_rec.fetch_add(1);
         }
     }
-    c.n_completed.fetch_add(1, std::memory_order_release);  // after the record is pushed
+    settle(record.correlation_id.external.value);                // after the record is queued
+    c.n_completed.fetch_add(1, std::memory_order_release);  // (the unmarked fallback's count)
+}
+
+int64_t env_int(const char* name, int64_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    char* end = nullptr;
+    const long long x = std::strtoll(v, &end, 10);
+    if (*end) {
+        std::fprintf(stderr, "nvrx capture: %s=%s is not an integer, using %lld\n", name, v, (long long)dflt);
+        return dflt;
+    }
+    return x;
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
@@ -274,16 +339,26 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
                                                        nullptr) != ROCPROFILER_STATUS_SUCCESS)
         return -1;
     if (rocprofiler_create_context(&c.disp_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
-    if (const char* k = std::getenv("NVRX_CAPTURE_RUNTIME_KERNELS")) c.keep_runtime = std::atoi(k) != 0;
-    {
+    c.keep_runtime = env_int("NVRX_CAPTURE_RUNTIME_KERNELS", 0) != 0;
+    c.flush_timeout_ms = std::max<int64_t>(1, env_int("NVRX_CAPTURE_FLUSH_TIMEOUT_MS", 1000));
+    if (env_int("NVRX_CAPTURE_MARKING", 1) != 0) {
         const rocprofiler_external_correlation_id_request_kind_t kinds[] = {
             ROCPROFILER_EXTERNAL_CORRELATION_REQUEST_KERNEL_DISPATCH};
-        c.self_marking = rocprofiler_configure_external_correlation_id_request_service(
-                             c.disp_ctx, kinds, 1, external_corr_request, nullptr) == ROCPROFILER_STATUS_SUCCESS;
+        c.marking = rocprofiler_configure_external_correlation_id_request_service(
+                        c.disp_ctx, kinds, 1, external_corr_request, nullptr) == ROCPROFILER_STATUS_SUCCESS;
     }
     if (const char* m = std::getenv("NVRX_CAPTURE_DELIVERY")) {
         const std::string v(m);
-        c.delivery = v == "buffer" ? 0 : v == "callback" ? 1 : 2;
+        if (v == "buffer") {
+            c.delivery = 0;
+        } else if (v == "callback") {
+            c.delivery = 1;
+        } else if (v == "callback_counted") {
+            c.delivery = 2;
+        } else {
+            std::fprintf(stderr, "nvrx capture: NVRX_CAPTURE_DELIVERY=%s is not buffer | callback | "
+                                 "callback_counted; using callback\n", m);
+        }
     }
     if (c.delivery != 0) {
         const rocprofiler_tracing_operation_t complete_only[] = {ROCPROFILER_KERNEL_DISPATCH_COMPLETE};
@@ -298,8 +373,8 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
         size_t watermark = 1u << 20;  // ~ the Detector's CUPTI bufferSize (1 MB, cupti.py:25)
         // NVRX_CAPTURE_WATERMARK overrides it, not below 64 KiB: with watermarks of a few KB
         // rocprofiler-sdk (ROCm 7.2) was measured to lose dispatch records (tools/diag_capture.py)
-        if (const char* w = std::getenv("NVRX_CAPTURE_WATERMARK"))
-            watermark = std::max<size_t>(std::strtoull(w, nullptr, 10), (size_t)64 << 10);
+        watermark = (size_t)std::max<int64_t>(env_int("NVRX_CAPTURE_WATERMARK", (int64_t)watermark),
+                                              (int64_t)64 << 10);
         if (rocprofiler_create_buffer(c.disp_ctx, 8u << 20, watermark, ROCPROFILER_BUFFER_POLICY_LOSSLESS,
                                       dispatch_buffer_cb, nullptr, &c.buffer) != ROCPROFILER_STATUS_SUCCESS)
             return -1;
@@ -334,6 +409,85 @@ rocprofiler_tool_configure_result_t* nvrx_tool_configure(uint32_t, const char*, 
     return &cfg;
 }
 
+// a wait that spins (yielding) for the first 200 us -- the usual case after a synchronize -- and
+// then sleeps in short steps, so a long wait does not take a core from the runtime's thread
+struct Backoff {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void pause() const {
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    bool expired(int64_t ms) const {
+        return std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms);
+    }
+};
+
+// The counted flush: open a new epoch, then wait until no earlier one is owed anything (buffer
+// delivery: flushing the buffer on every round, since its callback is what settles).  False on
+// timeout, after giving the owed epochs up.
+bool wait_owed(Capture& c) {
+    std::lock_guard<std::mutex> lk(c.flush_mu);
+    const uint64_t last = c.epoch.load(std::memory_order_relaxed);
+    c.owed[(last + 1) % kEpochs].store(0, std::memory_order_relaxed);  // reused slot: kEpochs ago
+    c.epoch.store(last + 1, std::memory_order_release);  // new enqueues count in the next epoch
+    if (c.delivery == 0) (void)rocprofiler_flush_buffer(c.buffer);
+    const Backoff b;
+    for (uint64_t e = c.settled; e <= last; ++e) {
+        while (c.owed[e % kEpochs].load(std::memory_order_acquire) > 0) {
+            if (b.expired(c.flush_timeout_ms)) {
+                int64_t lost = 0;
+                for (uint64_t f = e; f <= last; ++f)
+                    lost += std::max<int64_t>(0, c.owed[f % kEpochs].load());
+                c.n_abandoned.fetch_add((uint64_t)lost);
+                c.n_timeouts.fetch_add(1);
+                c.settled = last + 1;
+                return false;
+            }
+            b.pause();
+            if (c.delivery == 0) (void)rocprofiler_flush_buffer(c.buffer);
+        }
+    }
+    c.settled = last + 1;
+    c.n_counted_flush.fetch_add(1);
+    return true;
+}
+
+// Without the marking service nothing is counted at enqueue: callback_counted waits for the
+// ENQUEUE callbacks' count, callback for a 200 us quiet period after the last completion
+// (bounded; counted as quiet_flushes), buffer for rocprofiler_flush_buffer alone.
+bool wait_uncounted(Capture& c) {
+    c.n_quiet_flush.fetch_add(1);
+    if (c.delivery == 0) return rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS;
+    const Backoff b;
+    if (c.delivery == 2) {
+        const uint64_t want = c.n_enqueued.load();
+        while (c.n_completed.load(std::memory_order_acquire) < want) {
+            if (b.expired(c.flush_timeout_ms)) return false;
+            b.pause();
+        }
+        return true;
+    }
+    using clk = std::chrono::steady_clock;
+    uint64_t seen = c.n_completed.load(std::memory_order_acquire);
+    auto quiet = clk::now();
+    while (clk::now() - quiet < std::chrono::microseconds(200)) {
+        if (b.expired(20)) break;
+        const uint64_t now = c.n_completed.load(std::memory_order_acquire);
+        if (now != seen) seen = now, quiet = clk::now();
+        std::this_thread::yield();
+    }
+    return true;
+}
+
+// the calling thread's marking (capture_self_begin / _end nest on one thread)
+struct SelfMark {
+    int depth = 0;
+    int slot = -1;
+};
+thread_local SelfMark t_mark;
+
 }  // namespace
 
 namespace nvrx {
@@ -350,36 +504,10 @@ int capture_start(nvrx_profiler* p) {
 int capture_stop(nvrx_profiler* p) {
     Capture& c = cap();
     if (!c.ready) return 0;
-    // no flush here: records of kernels enqueued while started are delivered later (buffer
-    // watermark, get_stats / reset flush) and still counted, as CUPTI's are
+    // no flush here: records of kernels enqueued while started are delivered later and still
+    // counted, as CUPTI's are (their completions still arrive with the context stopped)
     (void)p;
     return rocprofiler_stop_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
-}
-
-// callback delivery: completions of dispatches that have finished on the device are processed by
-// the runtime's signal handler shortly after; wait for them -- for the counted enqueues exactly
-// (bounded: a kernel still running is delivered to a later report, as a CUPTI flush(0) leaves
-// it), else until no completion arrived for a quiet period
-bool wait_completions(Capture& c) {
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
-    if (c.delivery == 2) {
-        const uint64_t want = c.n_enqueued.load();
-        while (c.n_completed.load(std::memory_order_acquire) < want) {
-            if (clk::now() - t0 > std::chrono::milliseconds(20)) return true;
-            std::this_thread::yield();
-        }
-        return true;
-    }
-    uint64_t seen = c.n_completed.load(std::memory_order_acquire);
-    auto quiet = clk::now();
-    while (clk::now() - quiet < std::chrono::microseconds(200)) {
-        if (clk::now() - t0 > std::chrono::milliseconds(20)) break;
-        const uint64_t now = c.n_completed.load(std::memory_order_acquire);
-        if (now != seen) seen = now, quiet = clk::now();
-        std::this_thread::yield();
-    }
-    return true;
 }
 
 void capture_drain(nvrx_profiler* p) {
@@ -404,8 +532,7 @@ int capture_flush() {
     } drain;
     const auto t0 = std::chrono::steady_clock::now();
     c.flush_t0.store(t0.time_since_epoch().count());
-    const bool ok = c.delivery == 0 ? rocprofiler_flush_buffer(c.buffer) == ROCPROFILER_STATUS_SUCCESS
-                                    : wait_completions(c);
+    const bool ok = c.marking ? wait_owed(c) : wait_uncounted(c);
     const auto t1 = std::chrono::steady_clock::now();
     const int64_t last = c.last_cb_end.load();
     if (last >= c.flush_t0.load()) c.flush_tail_ns.fetch_add((uint64_t)(t1.time_since_epoch().count() - last));
@@ -415,16 +542,37 @@ int capture_flush() {
     return ok ? 0 : -1;
 }
 
+// Mark the calling thread's dispatches as the library's own until capture_self_end.  Each
+// thread has a slot of its own, so reports on two threads (get_stats on one, an external tracer's
+// ingest on another) never unmark each other.  False when marking is off or every slot is taken
+// (the caller then pauses the dispatch context instead).
 bool capture_self_begin() {
     Capture& c = cap();
-    if (!c.ready || !c.self_marking) return false;
+    if (!c.ready || !c.marking) return false;
+    if (t_mark.depth > 0) {
+        ++t_mark.depth;
+        return true;
+    }
     rocprofiler_thread_id_t tid = 0;
     if (rocprofiler_get_thread_id(&tid) != ROCPROFILER_STATUS_SUCCESS || tid == 0) return false;
-    c.self_tid.store(tid, std::memory_order_release);
-    return true;
+    for (int i = 0; i < kMarks; ++i) {
+        uint64_t free = 0;
+        if (c.marks[i].compare_exchange_strong(free, tid, std::memory_order_acq_rel)) {
+            c.n_marked.fetch_add(1, std::memory_order_release);
+            t_mark = {1, i};
+            return true;
+        }
+    }
+    return false;
 }
 
-void capture_self_end() { cap().self_tid.store(0, std::memory_order_release); }
+void capture_self_end() {
+    if (t_mark.depth == 0 || --t_mark.depth > 0) return;
+    Capture& c = cap();
+    c.marks[t_mark.slot].store(0, std::memory_order_release);
+    c.n_marked.fetch_sub(1, std::memory_order_release);
+    t_mark.slot = -1;
+}
 
 void capture_detach(nvrx_profiler* p) {
     Capture& c = cap();
@@ -474,12 +622,20 @@ int nvrx_capture_stats(nvrx_capture_counters* out) {
     out->flush_first_cb_ns = (int64_t)c.flush_first_cb_ns.load();
     out->flush_callbacks = (int64_t)c.flush_cbs.load();
     out->flush_tail_ns = (int64_t)c.flush_tail_ns.load();
+    out->enqueues_counted = (int64_t)c.n_requested.load();
+    out->counted_flushes = (int64_t)c.n_counted_flush.load();
+    out->quiet_flushes = (int64_t)c.n_quiet_flush.load();
+    out->flush_timeouts = (int64_t)c.n_timeouts.load();
+    out->owed_abandoned = (int64_t)c.n_abandoned.load();
+    out->delivery = c.ready ? c.delivery : -1;
+    out->marking = c.marking ? 1 : 0;
     return NVRX_OK;
 }
 
 int nvrx_capture_flush(void) {
     if (nvrx::capture_flush() != 0) {
-        nvrx::set_error("nvrx_capture_flush: rocprofiler_flush_buffer failed");
+        nvrx::set_error("nvrx_capture_flush: timed out waiting for owed dispatch records "
+                        "(NVRX_CAPTURE_FLUSH_TIMEOUT_MS); they join a later report");
         return NVRX_ERR_RUNTIME;
     }
     return NVRX_OK;

@@ -13,7 +13,7 @@ import threading
 from typing import Optional
 
 LIB_NAME = "libnvrx_hip.so"
-ABI_VERSION = 4  # include/nvrx_straggler.h NVRX_ABI_VERSION
+ABI_VERSION = 5  # include/nvrx_straggler.h NVRX_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 NVRX_OK = 0
@@ -60,7 +60,9 @@ class CaptureCounters(ctypes.Structure):
     _fields_ = [("callbacks", i64), ("headers", i64), ("dispatches", i64),
                 ("callback_ns", i64), ("flushes", i64), ("flush_ns", i64), ("runtime_kernels", i64),
                 ("own_kernels", i64), ("flush_first_cb_ns", i64), ("flush_callbacks", i64),
-                ("flush_tail_ns", i64)]
+                ("flush_tail_ns", i64), ("enqueues_counted", i64), ("counted_flushes", i64),
+                ("quiet_flushes", i64), ("flush_timeouts", i64), ("owed_abandoned", i64),
+                ("delivery", i32), ("marking", i32)]
 
 
 class ProfilerConfig(ctypes.Structure):

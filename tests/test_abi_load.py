@@ -31,7 +31,7 @@ def test_python_binding_covers_header():
 
 def test_lib_loads_and_reports_abi():
     L = _native.lib()
-    assert L.nvrx_abi_version() == _native.ABI_VERSION == 4
+    assert L.nvrx_abi_version() == _native.ABI_VERSION == 5
     cnt = ctypes.c_int(-1)
     # no HIP device in the CPU container: the call succeeds (0 devices) or reports HIP error
     rc = L.nvrx_device_count(ctypes.byref(cnt))
@@ -60,4 +60,7 @@ def test_capture_counters_without_capture():
     c = _native.CaptureCounters()
     assert _native.lib().nvrx_capture_stats(ctypes.byref(c)) == 0
     assert (c.callbacks, c.dispatches, c.flushes, c.callback_ns) == (0, 0, 0, 0)
+    assert (c.enqueues_counted, c.counted_flushes, c.flush_timeouts, c.delivery) == (0, 0, 0, -1)
+    # the C struct and the ctypes mirror agree on the layout (two int32 at the end)
+    assert ctypes.sizeof(c) == 16 * 8 + 2 * 4
     assert _native.lib().nvrx_capture_stats(None) == _native.NVRX_ERR_INVALID

@@ -1,0 +1,160 @@
+"""GPU: completeness of the report-time flush of the live capture (capture.cpp, "Flush
+completeness").  The reference drains every completed activity record before it computes
+statistics -- cuptiActivityFlushAll(0) inside getStats (CuptiProfiler.cpp:136-146), after the
+Detector's torch.cuda.synchronize() (straggler.py:234-243) -- so a report holds exactly the
+kernels launched in its interval.  rocprofiler-sdk hands completions over on the runtime's
+signal-handler thread, late when the host is loaded; the flush therefore waits for every job
+dispatch counted at enqueue.  These cases check it where a timing heuristic would fail:
+
+  * a known number of launches on two streams per interval, every host core kept busy by other
+    processes through generate_report: each interval's num_calls equal the launched counts
+    exactly, the next interval holds none of the previous one's records, no flush timed out;
+  * reports on two threads at once (an external tracer's ingest loop against get_stats) never
+    capture the library's own kernels as the job's (each thread is marked on its own).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "nvidia-resiliency-ext-x_amd")
+# mangled name of nvrx::stragglers_kernel(const double*, long, double, unsigned char*)
+STRAG = "_ZN4nvrx17stragglers_kernelEPKdldPh"
+
+
+def _child(code, env=None, timeout=300):
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, "-c", f"import sys; sys.path.insert(0, {PKG!r})\n" + code],
+                       capture_output=True, text=True, timeout=timeout, env=e)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][7:])
+
+
+LOADED = r"""
+import ctypes, json
+from nvidia_resiliency_ext.straggler import cupti, ops, _native
+cupti.enable_capture()  # before the first HIP call
+import torch
+from nvidia_resiliency_ext import straggler
+D, S = straggler.Detector, straggler.Statistic
+D.initialize(profiling_interval=1, report_time_interval=1e9)
+small = torch.rand(1000, dtype=torch.float64, device="cuda")    # 4 blocks of 256
+big = torch.rand(70000, dtype=torch.float64, device="cuda")     # 274 blocks
+m1 = torch.empty(1000, dtype=torch.uint8, device="cuda")
+m2 = torch.empty(70000, dtype=torch.uint8, device="cuda")
+s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+ops.stragglers(small, 0.5, out=m1); ops.stragglers(big, 0.5, out=m2)  # code objects loaded
+torch.cuda.synchronize()
+D.generate_report()
+c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
+got, want = [], []
+for it in range(8):
+    n1, n2 = 300 + 97 * it, 200 + 31 * it
+    with D.detection_section("work", profile_cuda=True):
+        for i in range(max(n1, n2)):  # interleaved on two streams, no synchronize
+            if i < n1:
+                ops.stragglers(small, 0.5, out=m1, stream=s1)
+            if i < n2:
+                ops.stragglers(big, 0.5, out=m2, stream=s2)
+    rep = D.generate_report()  # synchronize + get_stats (the counted flush) + reset
+    got.append({k: int(v[S.NUM]) for k, v in rep.local_kernel_summaries.items()})
+    want.append({STRAG + "_blk_256_1_1_grid_4_1_1": n1, STRAG + "_blk_256_1_1_grid_274_1_1": n2})
+c1 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c1))
+D.shutdown()
+d = lambda f: getattr(c1, f) - getattr(c0, f)
+print("RESULT " + json.dumps({"got": got, "want": want, "delivery": c1.delivery,
+      "marking": c1.marking, "counted": d("counted_flushes"), "quiet": d("quiet_flushes"),
+      "timeouts": d("flush_timeouts"), "abandoned": d("owed_abandoned"),
+      "enqueues": d("enqueues_counted"), "flush_ms": d("flush_ns") / 1e6 / max(1, d("flushes"))}))
+""".replace("STRAG", repr(STRAG))
+
+
+def _busy(n):
+    """n processes that keep a host core each busy (the box's CPU share is 16)."""
+    return [subprocess.Popen([sys.executable, "-c", "while True: pass"]) for _ in range(n)]
+
+
+def test_flush_is_complete_under_host_load():
+    ncpu = len(os.sched_getaffinity(0))
+    hogs = _busy(min(32, 2 * ncpu))
+    try:
+        out = _child(LOADED)
+    finally:
+        for h in hogs:
+            h.kill()
+        for h in hogs:
+            h.wait()
+    assert out["delivery"] == 1 and out["marking"] == 1, out  # the shipped default
+    for i, (g, w) in enumerate(zip(out["got"], out["want"])):
+        assert g == w, (i, g, w)  # exact per interval: none lost, none carried over
+    assert out["counted"] >= 8 and out["quiet"] == 0, out
+    assert out["timeouts"] == 0 and out["abandoned"] == 0, out
+    # every launch of the 8 intervals was counted at enqueue (the Detector's own kernels run
+    # with the profiler stopped, or marked)
+    assert out["enqueues"] == sum(sum(w.values()) for w in out["want"]), out
+
+
+TWO_THREADS = r"""
+import ctypes, json, threading
+from nvidia_resiliency_ext.straggler import cupti, ops, _native
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=8192, capture=True)
+p.initialize()
+p.start()
+names = ["ext_kernel_%d" % i for i in range(4)]
+slots = [p.register_kernel(n) for n in names]
+gen = p.generation
+recs = torch.tensor([[slots[i % 4], 1000 + i] for i in range(4096)], dtype=torch.int32, device="cuda")
+score = torch.rand(1000, dtype=torch.float64, device="cuda")
+m = torch.empty(1000, dtype=torch.uint8, device="cuda")
+torch.cuda.synchronize()
+c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
+N_INGEST, N_JOB = 400, 2000
+stop = threading.Event()
+def tracer():  # an external tracer's device ingest (the library's own copy kernel) on its own thread
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for _ in range(N_INGEST):
+            p.ingest(recs, s, generation=gen)
+    s.synchronize()
+def job():
+    for _ in range(N_JOB):
+        ops.stragglers(score, 0.5, out=m)
+    torch.cuda.synchronize()
+ts = [threading.Thread(target=tracer), threading.Thread(target=job)]
+for t in ts:
+    t.start()
+reports = 0
+while any(t.is_alive() for t in ts):  # get_stats (bucketing + statistics kernels) meanwhile
+    p.get_stats()
+    reports += 1
+for t in ts:
+    t.join()
+torch.cuda.synchronize()
+st = {k: v.num_calls for k, v in p.get_stats().items()}
+c1 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c1))
+p.stop()
+p.shutdown()
+print("RESULT " + json.dumps({"stats": st, "reports": reports, "own": c1.own_kernels - c0.own_kernels,
+                              "n_ingest": N_INGEST, "n_job": N_JOB}))
+"""
+
+
+def test_concurrent_reports_never_capture_own_kernels():
+    """one process-wide marked thread let a second report's end unmark the first's
+    kernels.  Ingest (own copy kernels) on one thread, get_stats on another, a job thread
+    launching: the summaries hold the job's kernel and the ingested names, nothing else."""
+    out = _child(TWO_THREADS)
+    st = out["stats"]
+    job_key = STRAG + "_blk_256_1_1_grid_4_1_1"
+    assert st.get(job_key) == out["n_job"], st
+    ingested = {k: v for k, v in st.items() if k.startswith("ext_kernel_")}
+    # 400 x 4096 records over 4 names: each ring keeps its last 8192
+    assert ingested == {f"ext_kernel_{i}": 8192 for i in range(4)}, ingested
+    assert set(st) == {job_key} | set(ingested), sorted(st)  # no kernel of the library's own
+    assert out["reports"] >= 2 and out["own"] > 0, out

@@ -24,13 +24,20 @@ def test_live_gpt2_capture_stats_match_oracle(tmp_path):
                RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     cmd = [sys.executable, os.path.join(ROOT, "tools", "live_gpt2.py"), "--layers", "2",
            "--batch", "2", "--seq", "256", "--warmup", "2", "--base-steps", "3", "--steps", "10",
-           "--report-every", "5", "--dump", str(dump), "--out", str(out)]
+           "--report-every", "5", "--count-check", "--dump", str(dump), "--out", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads(out.read_text())
     assert res["capture"] is True
     assert res["kernel_keys"] > 20 and res["records_per_report"] > 100
     assert res["gpu_relative_perf_scores"] == {"0": 1.0} or res["gpu_relative_perf_scores"] == {0: 1.0}
+    # completeness (no explicit flush before the reports): every 5-step window holds exactly
+    # 5 x each key's launches of a one-step window -- nothing lost, nothing carried over
+    step = res["step_counts"]
+    assert step and len(res["window_counts"]) == 2
+    for w in res["window_counts"]:
+        assert w == {k: 5 * n for k, n in step.items()}, \
+            {k: (w.get(k), 5 * step.get(k, 0)) for k in set(w) | set(step) if w.get(k) != 5 * step.get(k, 0)}
 
     d = np.load(dump)
     slots, ns = d["slots"], d["ns"]

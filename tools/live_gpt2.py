@@ -100,6 +100,9 @@ def main():
                     help="Detector.initialize(profiling_interval=...): profile every k-th step")
     ap.add_argument("--profile-cuda", type=int, default=1,
                     help="0: sections time the CPU only (isolates the capture's cost)")
+    ap.add_argument("--count-check", action="store_true",
+                    help="no explicit flush before the reports; record each report's per-key "
+                         "num_calls and those of a one-step window (capture completeness)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -166,6 +169,15 @@ def main():
         det_step()
     D.generate_report()
 
+    def counts(rep):
+        return {k: int(v[straggler.Statistic.NUM]) for k, v in rep.local_kernel_summaries.items()}
+
+    step_counts = None
+    window_counts = []
+    if a.count_check:  # a one-step window: the launches of one training step, per kernel key
+        det_step()
+        step_counts = counts(D.generate_report())
+
     reports = []
     t_flush = []
     t_flush2 = []
@@ -178,17 +190,19 @@ def main():
             slots, ns = prof.get_records()
             names = {int(s): prof.name_of(s) for s in np.unique(slots)}
             dump = (slots, ns, names)
-        torch.cuda.synchronize()
+        if not a.count_check:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            D.cupti_manager.cupti_ext.flush_capture()
+            t_flush.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            D.cupti_manager.cupti_ext.flush_capture()  # nothing left: the fixed cost of a flush
+            t_flush2.append(time.perf_counter() - t0)
         t0 = time.perf_counter()
-        D.cupti_manager.cupti_ext.flush_capture()
-        t_flush.append(time.perf_counter() - t0)
-        t0 = time.perf_counter()
-        D.cupti_manager.cupti_ext.flush_capture()  # nothing left: the fixed cost of a flush
-        t_flush2.append(time.perf_counter() - t0)
-        t0 = time.perf_counter()
-        rep = D.generate_report()
+        rep = D.generate_report()  # its own synchronize + counted flush
         t_rep = time.perf_counter() - t0
         reports.append((t_rep, rep))
+        window_counts.append(counts(rep))
         last_report = rep
     n_det = max(1, a.steps // a.report_every) * a.report_every
     t_det = det_time / n_det
@@ -225,8 +239,9 @@ def main():
             "records_per_report": nrec, "kernel_keys": len(local_ks or {}),
             "report_ms": [x * 1e3 for x in t_rep],
             "report_ms_median": float(np.median(t_rep)) * 1e3,
-            "capture_flush_ms_median": float(np.median(t_flush)) * 1e3,
-            "empty_flush_ms_median": float(np.median(t_flush2)) * 1e3,
+            "capture_flush_ms_median": float(np.median(t_flush)) * 1e3 if t_flush else None,
+            "empty_flush_ms_median": float(np.median(t_flush2)) * 1e3 if t_flush2 else None,
+            "step_counts": step_counts, "window_counts": window_counts if a.count_check else None,
             "start_stop_pair_us": t_pair * 1e6,
             "report_elapsed_field_ms": rep.generate_report_elapsed_time,
             "gpu_relative_perf_scores": dict(rep.gpu_relative_perf_scores),
