@@ -105,7 +105,6 @@ from nvidia_resiliency_ext.straggler import cupti, ops, _native
 import torch
 p = cupti.KernelProfiler(statsMaxLenPerKernel=8192, capture=True)
 p.initialize()
-p.start()
 names = ["ext_kernel_%d" % i for i in range(4)]
 slots = [p.register_kernel(n) for n in names]
 gen = p.generation
@@ -113,6 +112,7 @@ recs = torch.tensor([[slots[i % 4], 1000 + i] for i in range(4096)], dtype=torch
 score = torch.rand(1000, dtype=torch.float64, device="cuda")
 m = torch.empty(1000, dtype=torch.uint8, device="cuda")
 torch.cuda.synchronize()
+p.start()  # the inputs above were made before: only the threads' launches below count
 c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
 N_INGEST, N_JOB = 400, 2000
 stop = threading.Event()
