@@ -333,7 +333,10 @@ int64_t env_int(const char* name, int64_t dflt) {
 int tool_init(rocprofiler_client_finalize_t, void*) {
     Capture& c = cap();
     if (rocprofiler_create_context(&c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
-    if (rocprofiler_configure_callback_tracing_service(c.sym_ctx,
+    // NVRX_CAPTURE_SYMBOLS=0 (cost attribution only, tools/capture_cost.cpp): no code-object
+    // tracing -- every key is then "unknown_kernel_..." and runtime blits are not recognised
+    if (env_int("NVRX_CAPTURE_SYMBOLS", 1) != 0 &&
+        rocprofiler_configure_callback_tracing_service(c.sym_ctx,
                                                        ROCPROFILER_CALLBACK_TRACING_CODE_OBJECT,
                                                        nullptr, 0, code_object_cb,
                                                        nullptr) != ROCPROFILER_STATUS_SUCCESS)

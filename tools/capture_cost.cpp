@@ -7,7 +7,11 @@
 //   cycle    started for the dispatch loop, then stopped before the flush measurements (how
 //            Detector.generate_report finds it: between detection sections)
 // For "started" the library's own share is nvrx_capture_stats().callback_ns (time inside our
-// buffer callback), so (started - callback) is rocprofiler-sdk's interception alone.
+// delivery callback), so (started - callback) is rocprofiler-sdk's interception alone.  The
+// services are toggled by the environment, one process per setting (tools/gpu_r05_cost.sh):
+// NVRX_CAPTURE_DELIVERY (buffer | callback | callback_counted), NVRX_CAPTURE_MARKING=0 (no
+// external-correlation-id request: no self-marking, no enqueue count), NVRX_CAPTURE_SYMBOLS=0
+// (no code-object tracing).
 // Build: hipcc --offload-arch=gfx950 -O2 tools/capture_cost.cpp -I include
 //        -L nvidia-resiliency-ext-x_amd/nvidia_resiliency_ext/straggler -lnvrx_hip -Wl,-rpath,...
 // Output: one JSON line.
@@ -103,14 +107,19 @@ int main(int argc, char** argv) {
            "\"flush_us\": {\"0\": %.1f, \"100\": %.1f, \"1000\": %.1f, \"10000\": %.1f}, "
            "\"get_stats_us_first\": %.1f, \"get_stats_us\": %.1f, \"stop_us\": %.1f, \"kernels\": %lld, "
            "\"flushes\": %lld, \"flush_ms_total\": %.3f, \"delivery\": \"%s\", "
-           "\"flush_first_callback_us\": %.1f, \"flush_callbacks\": %.1f, \"flush_tail_us\": %.1f}\n",
+           "\"flush_first_callback_us\": %.1f, \"flush_callbacks\": %.1f, \"flush_tail_us\": %.1f, "
+           "\"marking\": %d, \"delivery_mode\": %d, \"symbols\": \"%s\", \"enqueues_counted\": %lld, "
+           "\"counted_flushes\": %lld, \"quiet_flushes\": %lld, \"flush_timeouts\": %lld}\n",
            mode, avail, n, (t1 - t0) / n, (t2 - t0) / n, (long long)(c1.dispatches - c0.dispatches),
            c1.dispatches > c0.dispatches ? (c1.callback_ns - c0.callback_ns) * 1e-3 / (double)(c1.dispatches - c0.dispatches) : 0.0,
            flush_us[0], flush_us[1], flush_us[2], flush_us[3], gs_us, gs2_us, stop_us, (long long)kernels,
            (long long)c2.flushes, c2.flush_ns * 1e-6,
-           getenv("NVRX_CAPTURE_DELIVERY") ? getenv("NVRX_CAPTURE_DELIVERY") : "buffer",
+           getenv("NVRX_CAPTURE_DELIVERY") ? getenv("NVRX_CAPTURE_DELIVERY") : "callback",
            (cf1.flush_first_cb_ns - cf0.flush_first_cb_ns) * 1e-3 / nf,
-           (cf1.flush_callbacks - cf0.flush_callbacks) / nf, (cf1.flush_tail_ns - cf0.flush_tail_ns) * 1e-3 / nf);
+           (cf1.flush_callbacks - cf0.flush_callbacks) / nf, (cf1.flush_tail_ns - cf0.flush_tail_ns) * 1e-3 / nf,
+           (int)c2.marking, (int)c2.delivery, getenv("NVRX_CAPTURE_SYMBOLS") ? getenv("NVRX_CAPTURE_SYMBOLS") : "1",
+           (long long)(c1.enqueues_counted - c0.enqueues_counted), (long long)c2.counted_flushes,
+           (long long)c2.quiet_flushes, (long long)c2.flush_timeouts);
     if (p) nvrx_profiler_destroy(p);
     return 0;
 }
