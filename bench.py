@@ -131,7 +131,44 @@ def warm(step, n_min: int, world: int) -> int:
     return n
 
 
-def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True):
+def phases_loop(rep, ns, s_push, g, steps, world, time_kernel):
+    """The N-GPU launch mode: per report the statistics phase (a HIP graph, or eager without
+    one) between two timing events, then the rest -- on N GPUs the shard's score partials, the
+    eager all_gather and the combine; on 1 GPU the scores graph.  Returns (last result, elapsed
+    s between barriers, mean statistics ms or None)."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    res = None
+    barrier(world)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if time_kernel:
+            ev[i][0].record()
+        if g is not None:
+            g.run_stats()
+        else:
+            rep.compute_stats(ns, s_push)
+        if time_kernel:
+            ev[i][1].record()
+        if g is not None:
+            res = g.run_rest()
+        else:
+            rep.compute_scores()
+            res = rep.land()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if time_kernel else None
+    return res, elapsed, kern_ms
+
+
+def phases_label(rep, g) -> str:
+    return ("eager" if g is None else
+            "hip_graph: statistics | score partials | eager all_gather | combine" if rep.exchange else
+            "hip_graph: statistics | rest")
+
+
+def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True, use_graph=True,
+               graph_phases=False):
     """Full reports on one configuration.  use_graph: every report replays HIP graphs of the
     same kernels (one graph launch instead of one host launch per operation) -- on 1 GPU two
     whole-report graphs in flight (MatrixReporter.pipelined), on N GPUs the stats graph, the
@@ -171,42 +208,31 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
                 ks.append(ms)
             barrier(world)
         keep = min(s_push, cap)
+        phases = None
+        if graph_phases:
+            # the N-GPU launch mode on this one GPU (same reporter, buffers and warm-up rule), so
+            # that a 1 -> N curve can compare like with like
+            g = rep.graph(ns, s_push)
+            warm(g.run, max(1, warmup), world)
+            res_p, el_p, km_p = phases_loop(rep, ns, s_push, g, steps, world, time_kernel)
+            phases = dict(elapsed=el_p, kern_ms=km_p, launch=phases_label(rep, g),
+                          sets=res_p.stragglers_relative)
         return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed,
                     kern_ms=float(np.mean(ks)) if ks else None,
                     samples=R * K_local * keep, nseg=R * K_local, keep=keep,
-                    launch="hip_graph: whole reports, two in flight")
+                    launch="hip_graph: whole reports, two in flight", phases=phases)
     # N GPUs: the statistics, the shard's score partials and the combine replay as HIP graphs;
     # only the all_gather of the partials between them is an eager collective
     g = rep.graph(ns, s_push) if use_graph else None
     if g is not None:
         warm(g.run, max(1, warmup), world)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
-    barrier(world)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        if time_kernel:
-            ev[i][0].record()
-        if g is not None:
-            g.run_stats()
-        else:
-            rep.compute_stats(ns, s_push)
-        if time_kernel:
-            ev[i][1].record()
-        if g is not None:
-            res = g.run_rest()
-        else:
-            rep.compute_scores()
-            res = rep.land()
-    barrier(world)
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if time_kernel else None
+    res, elapsed, kern_ms = phases_loop(rep, ns, s_push, g, steps, world, time_kernel)
     keep = min(s_push, cap)
-    launch = ("eager" if g is None else
-              "hip_graph: statistics | score partials | eager all_gather | combine" if rep.exchange else
-              "hip_graph: statistics | rest")
+    launch = phases_label(rep, g)
     return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed, kern_ms=kern_ms,
-                samples=R * K_local * keep, nseg=R * K_local, keep=keep, launch=launch)
+                samples=R * K_local * keep, nseg=R * K_local, keep=keep, launch=launch,
+                phases=dict(elapsed=elapsed, kern_ms=kern_ms, launch=launch,
+                            sets=res.stragglers_relative))
 
 
 def score_digest(res) -> dict:
@@ -418,7 +444,8 @@ def main():
 
     # ---------------- value: configs[1] per GPU, kernel-hash sharded (weak) ----------
     K_global = C2["K"] * world
-    r = run_config(C2, K_global, args.steps, args.warmup, world, rank, dev, use_graph=not args.no_graph)
+    r = run_config(C2, K_global, args.steps, args.warmup, world, rank, dev, use_graph=not args.no_graph,
+                   graph_phases=not args.no_graph)
     tmax = allreduce(r["elapsed"], torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
     total_samples = allreduce(float(r["samples"]), torch.distributed.ReduceOp.SUM if world > 1 else None,
                               world, dev)
@@ -437,6 +464,16 @@ def main():
                       if torch.distributed.is_available() and torch.distributed.is_initialized() else 1)
     sec_steps = max(10, args.steps // 2)  # the configs[2] / configs[3] legs
     launch_per_rank = gather_labels(r["launch"], world)
+    # the same workload in the N-GPU launch mode (on N > 1 it IS the timed loop above)
+    ph = r["phases"]
+    phases = None
+    if ph is not None:
+        tph = comm_max(ph["elapsed"], world, dev)
+        phases = dict(ms_per_step=tph / args.steps * 1e3, value=total_samples * args.steps / tph,
+                      launch=ph["launch"], launch_per_rank=gather_labels(ph["launch"], world),
+                      stats_kernel_ms=comm_max(ph["kern_ms"], world, dev) if ph["kern_ms"] else None,
+                      straggler_sets_exact=all_ranks(bool(np.array_equal(
+                          ph["sets"], synth.straggler_ranks(C2["R"]).astype(bool))), world, dev))
 
     # ---------------- secondary: report latency at 4096 ranks (strong) ---------------
     lat = None
@@ -539,6 +576,11 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup, "warmup_min_ms": WARMUP_MIN_MS,
             "ms_per_step": ms_per_step,
+            # the N-GPU launch mode's time per report on the same workload: on 1 GPU measured
+            # after the pipelined loop, on N GPUs equal to ms_per_step (a like-for-like 1 -> N
+            # curve reads this field; "graph_phases" holds its label and rate)
+            "ms_per_step_graph_phases": phases["ms_per_step"] if phases else None,
+            "graph_phases": phases,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -291,6 +291,10 @@ class ReportGraph:
         if stats is None:  # the statistics phase (record streams: MatrixReporter.graph_records)
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
         _warm_up(rep, stats)
+        # the captured statistics phase trusts col_ref as the previous report's scores epilogue
+        # left it (colref_ready at capture): replays must pair it with the scores (run_rest),
+        # which run_stats checks against the reporter's flag -- kept current by every replay
+        self._needs_clean = rep._colref_clean
         self.stats = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.stats):
             stats()
@@ -316,18 +320,28 @@ class ReportGraph:
                 rep.compute_scores()
                 rep.h_out.copy_(rep.out, non_blocking=True)
 
+    def _check_clean(self) -> None:
+        if self._needs_clean and not self.rep._colref_clean:
+            raise RuntimeError("ReportGraph: the statistics graph was captured to follow a scores "
+                               "phase (its epilogue re-initialises the column reference); the last "
+                               "statistics phase was not followed by run_rest()")
+
     def run_stats(self) -> None:
+        self._check_clean()
         self.stats.replay()
+        self.rep._colref_clean = False
 
     def run_rest(self) -> BatchResult:
         rep = self.rep
         if self.rest is None:  # N GPUs: partials graph, eager all_gather, combine graph
             self.partials.replay()
+            rep._colref_clean = rep._fuse_ref()
             rep._exchange()
             self.finalize.replay()
             _wait(rep.device)
             return rep._unpack()
         self.rest.replay()
+        rep._colref_clean = rep._fuse_ref()
         _wait(rep.device)
         return rep._unpack()
 
@@ -335,7 +349,9 @@ class ReportGraph:
         if self.full is None:
             self.run_stats()
             return self.run_rest()
+        self._check_clean()
         self.full.replay()
+        self.rep._colref_clean = self.rep._fuse_ref()
         _wait(self.rep.device)
         return self.rep._unpack()
 
@@ -392,6 +408,7 @@ class PipelinedReports:
         if stats is None:
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
         _warm_up(rep, stats)
+        self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
 
         def capture(with_stats: bool, rest: bool, k: int):
@@ -424,6 +441,9 @@ class PipelinedReports:
         """Queue the next report (at most two in flight: collect() the oldest first)."""
         if len(self.pending) == 2:
             raise RuntimeError("two reports in flight: collect() one first")
+        if self._needs_clean and not self.rep._colref_clean:
+            raise RuntimeError("PipelinedReports: an unpaired statistics phase (ReportGraph."
+                               "run_stats without run_rest) left the column reference in use")
         k = self.n & 1
         if timed:
             if not self.timing:
@@ -442,6 +462,7 @@ class PipelinedReports:
             self.rest[k].replay()
         else:
             self.full[k].replay()
+        self.rep._colref_clean = self.rep._fuse_ref()
         self.done[k].record()
         self.pending.append((k, timed))
         self.n += 1

@@ -72,8 +72,17 @@ def test_launcher_four_ranks_gloo_rehearsal():
     want = "hip_graph: statistics | score partials | eager all_gather | combine"
     assert cfg["launch_per_rank"] == [want] * 4 and lat["launch_per_rank"] == [want] * 4
     assert zipf["launch_per_rank"] == [want] * 4
+    # every point carries the N-GPU launch mode's time, labelled; on N > 1
+    # it is the headline loop itself
+    gp = line["graph_phases"]
+    assert gp["launch_per_rank"] == [want] * 4 and gp["straggler_sets_exact"] is True
+    assert line["ms_per_step_graph_phases"] == line["ms_per_step"]
     one = _run(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
     assert one["zipf_16384_ranks"]["launch_per_rank"] == ["hip_graph: whole reports, two in flight"]
+    assert one["config"]["launch"] == "hip_graph: whole reports, two in flight"
+    assert one["graph_phases"]["launch_per_rank"] == ["hip_graph: statistics | rest"]
+    assert one["graph_phases"]["straggler_sets_exact"] is True
+    assert one["ms_per_step_graph_phases"] > 0
     for leg in ("latency_4096_ranks", "zipf_16384_ranks"):
         a, b = line[leg]["scores"], one[leg]["scores"]
         assert a["stragglers_rel"] == b["stragglers_rel"], leg

@@ -130,3 +130,26 @@ def test_pipelined_records_matches_eager_reports(R):
         np.testing.assert_array_equal(w.stragglers_individual, g.stragglers_individual)
     for f in ("num", "min", "max", "med", "avg", "std"):
         assert torch.equal(getattr(a.stats, f).view(torch.int32), getattr(b.stats, f).view(torch.int32)), f
+
+
+def test_unpaired_statistics_replay_is_refused():
+    """a captured statistics graph trusts the column reference that the previous
+    report's scores epilogue re-initialised; replayed twice without its scores it would reuse a
+    stale reference.  The replay order is checked, and paired replays still match report()."""
+    R, K, S = 8, 64, 1000
+    ns = synth.synth_matrix(R, K, S, device="cuda")
+    rep = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
+    want = rep.report(ns, S)
+    g = rep.graph(ns, S)
+    pipe = rep.pipelined(ns, S)
+    g.run_stats()
+    with pytest.raises(RuntimeError):
+        g.run_stats()
+    with pytest.raises(RuntimeError):
+        g.run()
+    with pytest.raises(RuntimeError):
+        pipe.submit()
+    res = g.run_rest()  # pairs the first statistics phase: back in order
+    np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
+    for res in (g.run(), (pipe.submit(), pipe.collect()[0])[1]):
+        np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
