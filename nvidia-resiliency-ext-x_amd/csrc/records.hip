@@ -21,7 +21,6 @@
 //           step, same-slot lanes grouped with ballot (leader = lowest lane), occurrence
 //           index = cursor + mbcnt(group), kept iff occurrence >= count - keep.
 #include <stdlib.h>
-#include <string.h>
 
 #include <algorithm>
 
@@ -478,265 +477,6 @@ void records_bucket_kernel(
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Warp-specialised bucketing: one persistent workgroup per CU walks its
-// streams with two groups of waves working on two streams at once --
-//   RW "reader" waves: pass 1 (the LDS slot counts) of stream i + 1, into one of two count tables;
-//   SW "scatter" waves: the scans, pass 2 and the copy-out of stream i, from the other table,
-//                       re-reading stream i (read by the readers one iteration earlier: ~380 KB
-//                       per CU, ~97 MB chip-wide, inside the 256 MB Infinity Cache) instead of
-//                       holding it in registers and the LDS stash.
-// so the CU keeps reading HBM while it scans and scatters, which the one-stream-per-block kernel
-// above cannot (its phases run in series).  The two groups meet at one workgroup barrier per
-// iteration; the scatter group's own phase barriers are LDS arrival counters (group_sync).
-// Same outputs as records_bucket_kernel (single pass, no forced stable order).
-
-// a barrier for the `nwaves` waves of a group: a monotone LDS arrival counter, each wave waiting
-// until it reaches the wave's next target (every wave of the group calls it the same number of times)
-__device__ __forceinline__ void group_sync(uint32_t* ctr, uint32_t& target, uint32_t nwaves) {
-    target += nwaves;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane_id() == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-        __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// the records of a stream swept by NW waves together (wave w takes 1 KB step w of every NW), U
-// 16-byte loads in flight per lane; lanes past the end see the slot ~0 (no slot of any table)
-template <int NW, int U, bool NT, class F>
-__device__ __forceinline__ void sweep_stream(const nvrx_record* rs, int64_t n, int w, int lane, F&& f) {
-    if ((((uintptr_t)rs) & 15) == 0) {
-        const u32x4* q = (const u32x4*)rs;
-        const int64_t np = n >> 1;
-        for (int64_t b = 0; b < np; b += (int64_t)U * NW * 64) {
-            u32x4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t p = b + ((int64_t)u * NW + w) * 64 + lane;
-                v[u] = p < np ? (NT ? __builtin_nontemporal_load(q + p) : q[p]) : u32x4{~0u, 0u, ~0u, 0u};
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                f(nvrx_record{v[u].x, v[u].y});
-                f(nvrx_record{v[u].z, v[u].w});
-            }
-        }
-        if ((n & 1) && w == 0 && lane == 0) f(rs[n - 1]);
-    } else {
-        for (int64_t b = 0; b < n; b += (int64_t)U * NW * 64) {
-            nvrx_record v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t i = b + ((int64_t)u * NW + w) * 64 + lane;
-                v[u] = i < n ? rs[i] : nvrx_record{~0u, 0u};
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) f(v[u]);
-        }
-    }
-}
-
-#ifndef NVRX_RB_WS_U2  // pass-2 loads in flight per lane (scatter group)
-#define NVRX_RB_WS_U2 4
-#endif
-template <int RW, int SW>
-__global__ __launch_bounds__(64 * (RW + SW)) void records_bucket_ws_kernel(
-    const nvrx_record* __restrict__ recs, const int64_t* __restrict__ rec_off, int64_t nslots,
-    int64_t cap, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns, int32_t* counts,
-    int64_t stage_cap, uint32_t cold_max, nvrx_stats_soa tiny, int64_t seg_stride, int64_t t0,
-    int64_t nstreams) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* const cnt2 = lds;                 // [2][nslots] pushes per slot, double-buffered
-    uint32_t* const cur = lds + 2 * nslots;     // [nslots] scatter cursor / occurrence counter
-    uint32_t* const start = lds + 3 * nslots;   // [nslots] bucket start | RB_OVF
-    uint32_t* const stage = lds + ((4 * nslots + 3) & ~(int64_t)3);  // [stage_cap] cold buckets
-    __shared__ uint32_t wtot[3][SW];
-    __shared__ uint32_t any_ovf, gctr;
-    const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
-    const bool reader = wave < RW;
-    const int sw = wave - RW;                    // scatter wave index (scatter group only)
-    const int stid = (int)threadIdx.x - 64 * RW;  // scatter thread index
-    for (int64_t s = threadIdx.x; s < 2 * nslots; s += blockDim.x) cnt2[s] = 0u;
-    if (threadIdx.x == 0) gctr = 0u;
-    __syncthreads();
-    uint32_t gtarget = 0;
-    const int64_t G = gridDim.x;
-    const int64_t nmine = (nstreams - (int64_t)blockIdx.x + G - 1) / G;  // this block's streams
-    const auto keep_of = [&](uint32_t total) {
-        return (cap > 0 && total > (uint32_t)cap) ? (uint32_t)cap : total;
-    };
-    const bool staging = stage_cap > 0;
-    const auto tier_of = [&](uint32_t total) {
-        const uint32_t keep = keep_of(total);
-        if (!staging || keep != total || keep > cold_max) return 2;
-        return keep <= (uint32_t)RB_TINY ? 0 : 1;
-    };
-    // iteration i: the readers count the block's stream i, the scatter group places stream i - 1
-    for (int64_t i = 0; i <= nmine; ++i) {
-        if (reader) {
-            if (i < nmine) {
-                const int64_t t = t0 + (int64_t)blockIdx.x + i * G;
-                const int64_t r0 = rec_off[t];
-                uint32_t* cnt = cnt2 + (i & 1) * nslots;
-                sweep_stream<RW, (RW < 4 ? 16 : RB_UNROLL), false>(recs + r0, rec_off[t + 1] - r0, wave, lane,
-                                                    [&](const nvrx_record& r) {
-                                                        if (r.slot < (uint32_t)nslots) atomicAdd(&cnt[r.slot], 1u);
-                                                    });
-            }
-        } else if (i > 0) {
-            const int64_t t = t0 + (int64_t)blockIdx.x + (i - 1) * G;
-            uint32_t* cnt = cnt2 + ((i - 1) & 1) * nslots;
-            const int64_t r0 = rec_off[t];
-            const int64_t n = rec_off[t + 1] - r0;
-            const nvrx_record* rs = recs + r0;
-            const int64_t base = stream_base(rec_off, t, nslots);
-            uint32_t* out = out_ns + base;
-            // (a) chunk totals of the padded keeps per tier, every scatter wave on its own slots
-            const int64_t chunk = ((nslots + SW - 1) / SW + 63) & ~(int64_t)63;
-            const int64_t c_lo = min(nslots, chunk * sw), c_hi = min(nslots, c_lo + chunk);
-            {
-                uint32_t p0 = 0, p1 = 0, p2 = 0;
-                for (int64_t s = c_lo + lane; s < c_hi; s += 64) {
-                    const uint32_t total = cnt[s];
-                    const uint32_t padded = (keep_of(total) + 3u) & ~3u;
-                    const int tr = tier_of(total);
-                    p0 += tr == 0 ? padded : 0u;
-                    p1 += tr == 1 ? padded : 0u;
-                    p2 += tr == 2 ? padded : 0u;
-                }
-                p0 = wave_sum_u32(p0);
-                p1 = wave_sum_u32(p1);
-                p2 = wave_sum_u32(p2);
-                if (lane == 0) {
-                    wtot[0][sw] = p0;
-                    wtot[1][sw] = p1;
-                    wtot[2][sw] = p2;
-                }
-                if (stid == 0) any_ovf = 0u;
-            }
-            group_sync(&gctr, gtarget, SW);
-            // (b) the tier scans: bucket starts, pass 2's cursors, seg_off / seg_len / counts
-            uint32_t cold_total, tiny_end;
-            {
-                const uint32_t w0 = lane < SW ? wtot[0][lane] : 0u;
-                const uint32_t w1 = lane < SW ? wtot[1][lane] : 0u;
-                const uint32_t w2 = lane < SW ? wtot[2][lane] : 0u;
-                const uint32_t tiny_total = wave_sum_u32(w0);
-                tiny_end = tiny_total;
-                cold_total = tiny_total + wave_sum_u32(w1);
-                const uint32_t lim = (uint32_t)min((int64_t)cold_total, stage_cap);
-                bool overflow = false;
-                uint32_t carry0 = wave_sum_u32(lane < sw ? w0 : 0u);
-                uint32_t carry1 = tiny_total + wave_sum_u32(lane < sw ? w1 : 0u);
-                uint32_t carry2 = cold_total + wave_sum_u32(lane < sw ? w2 : 0u);
-                for (int64_t c = c_lo; c < c_hi; c += 64) {
-                    const int64_t s = c + lane;
-                    uint32_t keep = 0, total = 0;
-                    int k = 3;  // none
-                    if (s < c_hi) {
-                        total = cnt[s];
-                        keep = keep_of(total);
-                        k = tier_of(total);
-                    }
-                    const uint32_t padded = (keep + 3u) & ~3u;
-                    const uint32_t i0 = wave_incl_scan_u32(k == 0 ? padded : 0u);
-                    const uint32_t i1 = wave_incl_scan_u32(k == 1 ? padded : 0u);
-                    const uint32_t i2 = wave_incl_scan_u32(k == 2 ? padded : 0u);
-                    if (k < 3) {
-                        const uint32_t st = (k == 0 ? carry0 + i0 : k == 1 ? carry1 + i1 : carry2 + i2) - padded;
-                        const bool ovf = keep != total;
-                        overflow |= ovf;
-                        const uint32_t flag = ovf ? RB_OVF : 0u;
-                        start[s] = st | flag;
-                        cur[s] = flag ? RB_OVF : st;
-                        const int64_t g = t * seg_stride + s;
-                        const bool reduced = tiny.num && k == 0 && keep >= 1 && st + padded <= lim;
-                        if (!reduced || NVRX_RB_TINY_COPY) seg_off[g] = base + st;
-                        seg_len[g] = reduced ? -(int32_t)keep : (int32_t)keep;
-                        if (counts) counts[g] = (int32_t)total;
-                    }
-                    carry0 += __builtin_amdgcn_readlane(i0, 63);
-                    carry1 += __builtin_amdgcn_readlane(i1, 63);
-                    carry2 += __builtin_amdgcn_readlane(i2, 63);
-                }
-                if (__ballot(overflow) != 0 && lane == 0) any_ovf = 1u;
-            }
-            group_sync(&gctr, gtarget, SW);
-            // (c) pass 2: the stream again (the Infinity Cache's copy), one returning LDS atomic per
-            // record of a slot that kept everything; overflowed slots are left to (e)
-            const uint32_t stage_lim = (uint32_t)min((int64_t)cold_total, stage_cap);
-            sweep_stream<SW, NVRX_RB_WS_U2, true>(rs, n, sw, lane, [&](const nvrx_record& r) {
-                if (r.slot < (uint32_t)nslots) {
-                    const uint32_t pos = atomicAdd(&cur[r.slot], 1u);
-                    if (pos < stage_lim)
-                        stage[pos] = r.ns;
-                    else if (!(pos & RB_OVF))
-                        out[pos] = r.ns;
-                }
-            });
-            group_sync(&gctr, gtarget, SW);
-            // (d) the staged cold buckets out in 16-byte stores (past the tiny tier, which is reduced
-            // here from LDS and never read again), and the tiny buckets' statistics
-            if (stage_lim > 0) {
-                const u32x4* sv = (const u32x4*)stage;
-                u32x4* ov = (u32x4*)out;
-                const uint32_t skip = (tiny.num && !NVRX_RB_TINY_COPY && tiny_end <= stage_lim) ? tiny_end / 4 : 0u;
-                for (uint32_t j = skip + stid; j < stage_lim / 4; j += 64 * SW) ov[j] = sv[j];
-                if (tiny.num) {
-                    for (int64_t s = stid; s < nslots; s += 64 * SW) {
-                        const uint32_t total = cnt[s];
-                        const uint32_t keep = keep_of(total);
-                        const uint32_t st = start[s];
-                        if (tier_of(total) == 0 && keep >= 1 && st + ((keep + 3u) & ~3u) <= stage_lim) {
-                            const u32x4 a = sv[st / 4];
-                            const u32x4 b = keep > 4 ? sv[st / 4 + 1] : u32x4{~0u, ~0u, ~0u, ~0u};
-                            unsigned v[RB_TINY] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-                            lane_stats<RB_TINY>(v, (int)keep, t * seg_stride + s, tiny, ColRef{});
-                        }
-                    }
-                }
-            }
-            // (e) overflowed slots: scatter wave 0 walks the stream in push order, keeping each
-            // such slot's last `keep` records (the ring's), as records_bucket_kernel does
-            if (any_ovf && sw == 0) {
-                for (int64_t s = lane; s < nslots; s += 64)
-                    if (start[s] & RB_OVF) cur[s] = 0u;
-                __builtin_amdgcn_wave_barrier();
-                for (int64_t b = 0; b < n; b += 64) {
-                    const int64_t j = b + lane;
-                    nvrx_record rec = {0xFFFFFFFFu, 0u};
-                    if (j < n) rec = rs[j];
-                    const bool ok = rec.slot < (uint32_t)nslots && (start[rec.slot] & RB_OVF);
-                    uint64_t pending = __ballot(ok);
-                    uint32_t occ = 0;
-                    while (pending) {
-                        const int leader = __builtin_ffsll(pending) - 1;
-                        const uint32_t ls = __builtin_amdgcn_readlane(rec.slot, leader);
-                        const uint64_t grp = __ballot(ok && rec.slot == ls) & pending;
-                        const uint32_t c0 = cur[ls];
-                        if (ok && rec.slot == ls) occ = c0 + mbcnt(grp);
-                        __builtin_amdgcn_wave_barrier();
-                        if (lane == leader) cur[ls] = c0 + (uint32_t)__popcll(grp);
-                        __builtin_amdgcn_wave_barrier();
-                        pending &= ~grp;
-                    }
-                    if (ok) {
-                        const uint32_t keep = keep_of(cnt[rec.slot]);
-                        const uint32_t drop = cnt[rec.slot] - keep;
-                        if (occ >= drop) out[(start[rec.slot] & ~RB_OVF) + (occ - drop)] = rec.ns;
-                    }
-                }
-            }
-            group_sync(&gctr, gtarget, SW);
-            // (f) this count table is the readers' next-but-one
-            for (int64_t s = stid; s < nslots; s += 64 * SW) cnt[s] = 0u;
-        }
-        __syncthreads();
-    }
-}
-
 int64_t records_bucket_capacity(int64_t n, int64_t nstreams, int64_t nslots) {
     int64_t c = 0;
     for (int64_t lo = 0; lo < nslots; lo += RB_PASS_SLOTS) {
@@ -780,81 +520,12 @@ constexpr int RB_COLD = NVRX_RB_COLD;  // largest cold bucket (records)
 constexpr int RB_WAVES = NVRX_RB_WAVES;
 constexpr int RB_REGS = RB_REGS_PER_BLOCK / (64 * RB_WAVES);
 
-// The warp-specialised kernel's launch: one persistent workgroup per CU.  NVRX_RB_WS = "RWxSW"
-// (4x12, 6x10, 8x8) selects it and its split, NVRX_RB_WS_STAGE_KB its cold-bucket stage; read at
-// every launch (a captured graph keeps the choice it was captured with).
-template <int RW, int SW>
-static hipError_t launch_ws(const nvrx_record* recs, const int64_t* rec_off, int64_t t0, int64_t nlaunch,
-                            int64_t nslots, int64_t cap, int64_t* seg_off, int32_t* seg_len,
-                            uint32_t* out_ns, int32_t* counts, hipStream_t st, const nvrx_stats_soa& tiny,
-                            int64_t seg_stride) {
-    const void* k = (const void*)records_bucket_ws_kernel<RW, SW>;
-    static size_t attr_lds = 0;
-    static int ncu = 0;
-    static size_t static_lds = 0;
-    if (attr_lds == 0) {
-        hipFuncAttributes fa;
-        hipError_t e = hipFuncGetAttributes(&fa, k);
-        if (e != hipSuccess) return e;
-        static_lds = fa.sharedSizeBytes;
-        int dev = 0;
-        e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-        const size_t lds = 160 * 1024 - ((static_lds + 255) & ~(size_t)255);
-        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr_lds = lds;
-    }
-    const size_t counters = (size_t)((4 * nslots + 3) & ~(int64_t)3) * sizeof(uint32_t);
-    if (counters > attr_lds) return hipErrorInvalidValue;
-    int64_t stage_kb = RB_STAGE_KB;
-    if (const char* e = getenv("NVRX_RB_WS_STAGE_KB")) stage_kb = atoi(e);
-    const int64_t stage_cap =
-        std::min<int64_t>(stage_kb * 256, (int64_t)(attr_lds - counters) / 4) & ~(int64_t)3;
-    const size_t lds = counters + (size_t)stage_cap * 4;
-    const int64_t grid = std::min<int64_t>(nlaunch, std::max(ncu, 1));
-    hipLaunchKernelGGL((records_bucket_ws_kernel<RW, SW>), dim3((unsigned)grid), dim3(64 * (RW + SW)), lds, st,
-                       recs, rec_off, nslots, cap, seg_off, seg_len, out_ns, counts, stage_cap,
-                       (uint32_t)RB_COLD, tiny, seg_stride, t0, nlaunch);
-    return hipGetLastError();
-}
-
-static int ws_split() {  // 0: classic kernel
-    const char* e = getenv("NVRX_RB_WS");
-    if (!e || !*e || !strcmp(e, "0")) return 0;
-    if (!strcmp(e, "4x12")) return 412;
-    if (!strcmp(e, "6x10")) return 610;
-    if (!strcmp(e, "8x8")) return 88;
-    if (!strcmp(e, "2x14")) return 214;
-    if (!strcmp(e, "3x13")) return 313;
-    return 0;
-}
-
 static hipError_t records_bucket_pass(const nvrx_record* recs, const int64_t* rec_off, int64_t t0,
                                       int64_t nlaunch, int64_t nstreams, int64_t nslots, int64_t cap,
                                       int force_stable, int64_t* seg_off, int32_t* seg_len, uint32_t* out_ns,
                                       int32_t* counts, hipStream_t st, const nvrx_stats_soa* tiny,
                                       uint32_t slot_lo, int64_t seg_stride, int pass) {
     if (nlaunch <= 0 || nslots <= 0) return hipSuccess;
-    if (const int ws = ws_split(); ws && pass == 0 && slot_lo == 0 && !force_stable &&
-                                   (size_t)nslots * 16 <= 64 * 1024) {
-        const nvrx_stats_soa tsoa = tiny ? *tiny : nvrx_stats_soa{};
-        if (ws == 412)
-            return launch_ws<4, 12>(recs, rec_off, t0, nlaunch, nslots, cap, seg_off, seg_len, out_ns, counts,
-                                    st, tsoa, seg_stride);
-        if (ws == 610)
-            return launch_ws<6, 10>(recs, rec_off, t0, nlaunch, nslots, cap, seg_off, seg_len, out_ns, counts,
-                                    st, tsoa, seg_stride);
-        if (ws == 214)
-            return launch_ws<2, 14>(recs, rec_off, t0, nlaunch, nslots, cap, seg_off, seg_len, out_ns, counts,
-                                    st, tsoa, seg_stride);
-        if (ws == 313)
-            return launch_ws<3, 13>(recs, rec_off, t0, nlaunch, nslots, cap, seg_off, seg_len, out_ns, counts,
-                                    st, tsoa, seg_stride);
-        return launch_ws<8, 8>(recs, rec_off, t0, nlaunch, nslots, cap, seg_off, seg_len, out_ns, counts,
-                               st, tsoa, seg_stride);
-    }
     const size_t lds = (size_t)nslots * 3 * sizeof(uint32_t);
     if (lds > NVRX_RECORDS_MAX_LDS) return hipErrorInvalidValue;
     const nvrx_stats_soa tiny_soa = tiny ? *tiny : nvrx_stats_soa{};
