@@ -58,7 +58,10 @@ extern "C" {
 
 /* largest retained segment (statsMaxLenPerKernel) the kernels accept.  The reference's ring takes
  * any capacity (CuptiProfiler.h:49-51); rings of up to 32,768 samples are sorted on chip, longer
- * ones in device scratch (slower, same bits). */
+ * ones in device scratch (slower, same bits): 4 B per retained sample of every segment in flight,
+ * up to 256 MiB per launch and, near 2^30, 4 GiB for one segment's workgroup.  Freed scratch above
+ * 256 MiB returns to the driver at the next synchronisation.  Practical rings are <= 2^24 samples
+ * (nvrx_profiler_create warns above that). */
 #define NVRX_MAX_SEGMENT (1 << 30)
 
 /* SoA output of the statistics kernels: one entry per segment (device pointers).

@@ -537,6 +537,11 @@ int nvrx_profiler_create(const nvrx_profiler_config* cfg, nvrx_profiler** out) {
                    "nvrx_profiler_create: statsMaxLenPerKernel must be in [1, 2^30]");
     NVRX_CHECK_ARG(cfg->mode == NVRX_STATS_FAST || cfg->mode == NVRX_STATS_EXACT,
                    "nvrx_profiler_create: unknown mode");
+    if (cfg->stats_max_len_per_kernel > ((int64_t)1 << 24))
+        std::fprintf(stderr, "nvrx_profiler_create: statsMaxLenPerKernel=%lld: rings above 2^24 samples "
+                             "are reduced in device scratch of up to 4 B per retained sample (4 GiB at "
+                             "2^30) by one workgroup per kernel -- slow\n",
+                     (long long)cfg->stats_max_len_per_kernel);
     std::lock_guard<std::mutex> lk(g_instance_mu);
     if (g_instance)  // CuptiProfiler.cpp:86-87
         return fail(NVRX_ERR_SINGLETON, "Only one CuptiProfiler instance is allowed.");

@@ -128,7 +128,7 @@ hipError_t section_stats(const double* vals, const int64_t* off, int64_t nsec, i
         const int64_t per = std::max<int64_t>(1, ((int64_t)256 << 20) / (np2 * (int64_t)sizeof(double)));
         const int64_t chunk = std::min(nsec, per);
         void* work = nullptr;
-        hipError_t e = hipMallocAsync(&work, (size_t)(chunk * np2) * sizeof(double), st);
+        hipError_t e = scratch_alloc(&work, (size_t)(chunk * np2) * sizeof(double), st);
         if (e != hipSuccess) return e;
         for (int64_t c0 = 0; c0 < nsec && e == hipSuccess; c0 += chunk) {
             const int64_t m = std::min(chunk, nsec - c0);

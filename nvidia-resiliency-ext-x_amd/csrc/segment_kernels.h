@@ -1212,7 +1212,7 @@ static hipError_t launch_exact(const Segs& segs, int64_t nseg, int64_t max_len,
         // longer rings: device scratch, the batch in chunks of blocks (one slice each)
         const int64_t np2 = exact_global_np2(max_len), chunk = exact_global_blocks(np2, nseg);
         void* work = nullptr;
-        hipError_t e = hipMallocAsync(&work, (size_t)(chunk * np2) * sizeof(float), st);
+        hipError_t e = scratch_alloc(&work, (size_t)(chunk * np2) * sizeof(float), st);
         if (e != hipSuccess) return e;
         for (int64_t s0 = 0; s0 < nseg && e == hipSuccess; s0 += chunk) {
             hipLaunchKernelGGL((seg_stats_exact_global_kernel<Segs>), dim3((unsigned)std::min(chunk, nseg - s0)),

@@ -24,6 +24,25 @@
 
 namespace nvrx {
 
+// (nvrx_internal.h) the default pool's release threshold is raised once, to a cap: freed scratch
+// up to NVRX_SCRATCH_KEEP_BYTES stays reserved for the next report; above it (the long-ring
+// paths: up to 4 B per retained sample of the segments in flight) it is released at the next
+// synchronisation instead of staying taken from the training job
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+    static std::once_flag once[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        std::call_once(once[dev], [dev] {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t thr = NVRX_SCRATCH_KEEP_BYTES;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+        });
+    }
+    return hipMallocAsync(p, bytes, st);
+}
+
 using namespace ragged;
 
 // The class kernels are dealt over the caller's stream and one side stream per device

@@ -390,23 +390,6 @@ int cu_count() {
     return cus[dev];
 }
 
-// Stream-ordered scratch from the device's default pool; the pool keeps freed blocks
-// (release threshold raised once) so steady-state reports do not return to the driver.
-hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
-    static std::once_flag once[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        std::call_once(once[dev], [dev] {
-            hipMemPool_t pool;
-            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-                uint64_t thr = UINT64_MAX;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-            }
-        });
-    }
-    return hipMallocAsync(p, bytes, st);
-}
-
 template <int N>
 void launch_lane(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls, bool aligned16,
                  const nvrx_stats_soa& out, hipStream_t st) {
