@@ -32,7 +32,14 @@
 // rocprofiler-sdk tools configure when the ROCm runtime initialises: nvrx_capture_configure
 // must run before the process's first HIP call (the Python side does it at
 // KernelProfiler(capture=True) construction and reports whether it took effect).
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+// the installed hsa_api_trace.h names its sibling headers "inc/..." unless built as part of the runtime
+#define AMD_INTERNAL_BUILD
+#include <hsa/hsa_api_trace.h>
+#undef AMD_INTERNAL_BUILD
 #include <rocprofiler-sdk/external_correlation.h>
+#include <rocprofiler-sdk/intercept_table.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
@@ -103,6 +110,22 @@ struct Capture {
     int64_t flush_timeout_ms = 1000;
     std::atomic<uint64_t> n_requested{0}, n_counted_flush{0}, n_quiet_flush{0}, n_timeouts{0},
         n_abandoned{0};
+    // queue delivery (3, see "Queue delivery" below): every kernel dispatch packet of an
+    // intercepted queue gets a completion signal of ours while started; pending = dispatches not
+    // harvested yet (enqueue order), pool = free signals (value 1); both under pmu
+    struct Pending {
+        hsa_signal_t sig;
+        hsa_agent_t agent;
+        uint64_t obj;  // kernel_object of the packet
+        uint32_t bx, by, bz, gx, gy, gz;
+    };
+    std::mutex pmu;
+    std::vector<Pending> pending;
+    std::vector<hsa_signal_t> pool;
+    std::atomic<bool> qactive{false};     // the profiler is started
+    std::atomic<bool> q_installed{false}; // hsa_queue_create is ours
+    std::atomic<uint64_t> n_queues{0}, n_signals{0}, n_signal_fail{0}, n_chained{0};
+    double tick_ns = 0.0;                 // ns per HSA system timestamp tick (first harvest)
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -110,6 +133,13 @@ Capture& cap() {
     static Capture c;
     return c;
 }
+
+// the calling thread's marking (capture_self_begin / _end nest on one thread)
+struct SelfMark {
+    int depth = 0;
+    int slot = -1;
+};
+thread_local SelfMark t_mark;
 
 void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_user_data_t*,
                     void*) {
@@ -122,6 +152,7 @@ void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_us
     std::string n = d->kernel_name ? d->kernel_name : "";
     if (n.size() > 3 && n.compare(n.size() - 3, 3, ".kd") == 0) n.resize(n.size() - 3);
     std::lock_guard<std::mutex> lk(cap().mu);
+    cap().names[d->kernel_object] = n;  // queue delivery keys dispatches by the packet's kernel_object
     cap().names[d->kernel_id] = std::move(n);
 }
 
@@ -318,6 +349,215 @@ void dispatch_callback_cb(rocprofiler_callback_tracing_record_t record, rocprofi
     c.n_completed.fetch_add(1, std::memory_order_release);  // (the unmarked fallback's count)
 }
 
+// ------------------------------------------------------------------------------- queue delivery
+// NVRX_CAPTURE_DELIVERY=queue: no rocprofiler-sdk dispatch tracing at all.  Through
+// rocprofiler-sdk's intercept-table service the library takes hsa_queue_create: every queue the
+// HIP runtime creates is an HSA intercept queue with profiling enabled, and while the profiler is
+// started each kernel dispatch packet (on a thread that is not running a report of ours) gets a
+// completion signal from a pool -- the CP then writes the kernel's start / end timestamps into it.
+// Nothing runs per completion: a flush (and stop) harvests, in enqueue order, every pending
+// dispatch whose signal has reached 0 -- exactly the kernels that completed, as
+// cuptiActivityFlushAll(0) delivers them (CuptiProfiler.cpp:138) -- reads its timestamps
+// (hsa_amd_profiling_get_dispatch_time) and returns the signal to the pool.  A packet that
+// carried a completion signal of its own keeps it through a barrier-AND packet right behind it
+// (barrier bit set: it completes once the kernel has, and signals the original).
+struct QueueFns {
+    decltype(hsa_queue_create)* queue_create = nullptr;
+    decltype(hsa_amd_queue_intercept_create)* icreate = nullptr;
+    decltype(hsa_amd_queue_intercept_register)* iregister = nullptr;
+    decltype(hsa_amd_profiling_set_profiler_enabled)* prof_enable = nullptr;
+    decltype(hsa_amd_profiling_get_dispatch_time)* dispatch_time = nullptr;
+    decltype(hsa_amd_signal_create)* signal_create = nullptr;
+    decltype(hsa_signal_load_scacquire)* load = nullptr;
+    decltype(hsa_signal_store_relaxed)* store = nullptr;
+    decltype(hsa_system_get_info)* sys_info = nullptr;
+};
+QueueFns qf;
+
+struct QueueInfo {
+    hsa_agent_t agent;
+};
+
+constexpr uint16_t packet_type(uint16_t header) {
+    return (uint16_t)((header >> HSA_PACKET_HEADER_TYPE) & ((1u << HSA_PACKET_HEADER_WIDTH_TYPE) - 1));
+}
+
+// runs on the thread that rings the queue's doorbell (the launching thread under HIP's direct
+// dispatch), for every batch of packets written to an intercepted queue
+void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
+                 hsa_amd_queue_intercept_packet_writer writer) {
+    Capture& c = cap();
+    if (!c.qactive.load(std::memory_order_acquire)) {
+        writer(pkts, n);
+        return;
+    }
+    const auto* in = static_cast<const hsa_kernel_dispatch_packet_t*>(pkts);
+    uint64_t nk = 0;
+    for (uint64_t i = 0; i < n; ++i) nk += packet_type(in[i].header) == HSA_PACKET_TYPE_KERNEL_DISPATCH;
+    if (nk == 0 || t_mark.depth > 0) {  // t_mark: a report of ours runs on this thread -- not captured
+        if (t_mark.depth > 0) c.n_own.fetch_add(nk, std::memory_order_relaxed);
+        writer(pkts, n);
+        return;
+    }
+    const hsa_agent_t agent = static_cast<const QueueInfo*>(data)->agent;
+    thread_local std::vector<hsa_signal_t> sigs;
+    sigs.assign(nk, hsa_signal_t{0});
+    {
+        std::lock_guard<std::mutex> lk(c.pmu);
+        uint64_t j = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (packet_type(in[i].header) != HSA_PACKET_TYPE_KERNEL_DISPATCH) continue;
+            if (c.pool.empty()) {  // grow (rare: the pool keeps what reports returned)
+                for (int g = 0; g < 256; ++g) {
+                    hsa_signal_t s{0};
+                    if (qf.signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &s) != HSA_STATUS_SUCCESS) break;
+                    c.pool.push_back(s);
+                }
+                if (c.pool.empty()) break;
+            }
+            const hsa_signal_t s = c.pool.back();
+            c.pool.pop_back();
+            sigs[j++] = s;
+            const hsa_kernel_dispatch_packet_t& k = in[i];
+            c.pending.push_back({s, agent, k.kernel_object, k.workgroup_size_x, k.workgroup_size_y,
+                                 k.workgroup_size_z, k.grid_size_x, k.grid_size_y, k.grid_size_z});
+        }
+    }
+    thread_local std::vector<hsa_kernel_dispatch_packet_t> out;  // 64-byte AQL slots
+    out.clear();
+    uint64_t j = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (packet_type(in[i].header) != HSA_PACKET_TYPE_KERNEL_DISPATCH || sigs[j].handle == 0) {
+            if (packet_type(in[i].header) == HSA_PACKET_TYPE_KERNEL_DISPATCH) {
+                ++j;
+                c.n_signal_fail.fetch_add(1, std::memory_order_relaxed);
+            }
+            out.push_back(in[i]);
+            continue;
+        }
+        hsa_kernel_dispatch_packet_t k = in[i];
+        const hsa_signal_t orig = k.completion_signal;
+        k.completion_signal = sigs[j++];
+        out.push_back(k);
+        if (orig.handle != 0) {  // the packet's own signal, behind it
+            hsa_barrier_and_packet_t b{};
+            const uint16_t release = (uint16_t)((k.header >> HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) &
+                                                ((1u << HSA_PACKET_HEADER_WIDTH_SCRELEASE_FENCE_SCOPE) - 1));
+            b.header = (uint16_t)((HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) |
+                                  (1u << HSA_PACKET_HEADER_BARRIER) |
+                                  (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                  (release << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
+            b.completion_signal = orig;
+            hsa_kernel_dispatch_packet_t slot;
+            static_assert(sizeof(slot) == sizeof(b), "AQL packets are 64 bytes");
+            std::memcpy(&slot, &b, sizeof(b));
+            out.push_back(slot);
+            c.n_chained.fetch_add(1, std::memory_order_relaxed);
+        }
+    }
+    c.n_signals.fetch_add(nk, std::memory_order_relaxed);
+    c.n_requested.fetch_add(nk, std::memory_order_relaxed);
+    writer(out.data(), out.size());
+}
+
+hsa_status_t q_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
+                      void (*callback)(hsa_status_t, hsa_queue_t*, void*), void* data,
+                      uint32_t private_segment_size, uint32_t group_segment_size, hsa_queue_t** queue) {
+    const hsa_status_t st = qf.icreate(agent, size, type, callback, data, private_segment_size,
+                                       group_segment_size, queue);
+    if (st != HSA_STATUS_SUCCESS)  // not interceptable: a plain queue, not captured
+        return qf.queue_create(agent, size, type, callback, data, private_segment_size, group_segment_size,
+                               queue);
+    auto* qi = new QueueInfo{agent};  // queues live as long as the process: a few bytes each
+    if (qf.iregister(*queue, q_intercept, qi) != HSA_STATUS_SUCCESS ||
+        qf.prof_enable(*queue, 1) != HSA_STATUS_SUCCESS)
+        std::fprintf(stderr, "nvrx capture: could not intercept an HSA queue; its kernels are not captured\n");
+    cap().n_queues.fetch_add(1);
+    return st;
+}
+
+// rocprofiler-sdk hands over the HSA API table as the runtime initialises
+void hsa_table_cb(rocprofiler_intercept_table_t type, uint64_t, uint64_t, void** tables, uint64_t num,
+                  void*) {
+    if (type != ROCPROFILER_HSA_TABLE || num == 0 || !tables[0]) return;
+    auto* t = static_cast<HsaApiTable*>(tables[0]);
+    qf.queue_create = t->core_->hsa_queue_create_fn;
+    qf.icreate = t->amd_ext_->hsa_amd_queue_intercept_create_fn;
+    qf.iregister = t->amd_ext_->hsa_amd_queue_intercept_register_fn;
+    qf.prof_enable = t->amd_ext_->hsa_amd_profiling_set_profiler_enabled_fn;
+    qf.dispatch_time = t->amd_ext_->hsa_amd_profiling_get_dispatch_time_fn;
+    qf.signal_create = t->amd_ext_->hsa_amd_signal_create_fn;
+    qf.load = t->core_->hsa_signal_load_scacquire_fn;
+    qf.store = t->core_->hsa_signal_store_relaxed_fn;
+    qf.sys_info = t->core_->hsa_system_get_info_fn;
+    if (!qf.queue_create || !qf.icreate || !qf.iregister || !qf.prof_enable || !qf.dispatch_time ||
+        !qf.signal_create || !qf.load || !qf.store || !qf.sys_info)
+        return;
+    t->core_->hsa_queue_create_fn = q_create;
+    cap().q_installed = true;
+}
+
+// the completed pending dispatches, in enqueue order, into p (or dropped without one); the
+// signals go back to the pool
+void q_harvest(nvrx_profiler* p) {
+    Capture& c = cap();
+    if (!c.q_installed) return;
+    thread_local std::vector<Capture::Pending> done;
+    thread_local std::vector<nvrx::DispatchRec> batch;
+    done.clear();
+    batch.clear();
+    {
+        std::lock_guard<std::mutex> lk(c.pmu);
+        size_t w = 0;
+        for (size_t i = 0; i < c.pending.size(); ++i) {
+            if (qf.load(c.pending[i].sig) == 0)
+                done.push_back(c.pending[i]);
+            else
+                c.pending[w++] = c.pending[i];
+        }
+        c.pending.resize(w);
+    }
+    if (done.empty()) return;
+    if (c.tick_ns == 0.0) {
+        uint64_t f = 0;
+        c.tick_ns = qf.sys_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f
+                        ? 1e9 / (double)f : 1.0;
+    }
+    uint64_t runtime = 0;
+    for (const auto& e : done) {
+        hsa_amd_profiling_dispatch_time_t tm{0, 0};
+        (void)qf.dispatch_time(e.agent, e.sig, &tm);
+        rocprofiler_kernel_dispatch_info_t di{};
+        di.kernel_id = e.obj;
+        di.workgroup_size = {e.bx, e.by, e.bz};
+        di.grid_size = {e.gx, e.gy, e.gz};
+        const uint64_t ns = tm.end > tm.start
+                                ? (c.tick_ns == 1.0 ? tm.end - tm.start
+                                                    : (uint64_t)((double)(tm.end - tm.start) * c.tick_ns + 0.5))
+                                : 0;
+        nvrx::DispatchRec d;
+        switch (to_dispatch(di, 0, ns, 0, d)) {
+            case Kind::runtime: ++runtime; break;
+            case Kind::job: batch.push_back(d); break;
+            case Kind::own: break;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(c.pmu);
+        for (const auto& e : done) {
+            qf.store(e.sig, 1);
+            c.pool.push_back(e.sig);
+        }
+    }
+    c.n_cb.fetch_add(1);
+    c.n_rec.fetch_add(done.size());
+    c.n_completed.fetch_add(done.size(), std::memory_order_release);
+    c.n_runtime.fetch_add(runtime);
+    if (!p || batch.empty()) return;
+    c.n_pushed.fetch_add(batch.size());
+    nvrx::profiler_push_dispatches(p, batch.data(), batch.size(), composite_name);
+}
+
 int64_t env_int(const char* name, int64_t dflt) {
     const char* v = std::getenv(name);
     if (!v || !*v) return dflt;
@@ -344,24 +584,16 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
     if (rocprofiler_create_context(&c.disp_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
     c.keep_runtime = env_int("NVRX_CAPTURE_RUNTIME_KERNELS", 0) != 0;
     c.flush_timeout_ms = std::max<int64_t>(1, env_int("NVRX_CAPTURE_FLUSH_TIMEOUT_MS", 1000));
+    if (c.delivery == 3) {  // queue delivery: no dispatch tracing service (hsa_table_cb does the work)
+        if (rocprofiler_start_context(c.sym_ctx) != ROCPROFILER_STATUS_SUCCESS) return -1;
+        c.ready = true;
+        return 0;
+    }
     if (env_int("NVRX_CAPTURE_MARKING", 1) != 0) {
         const rocprofiler_external_correlation_id_request_kind_t kinds[] = {
             ROCPROFILER_EXTERNAL_CORRELATION_REQUEST_KERNEL_DISPATCH};
         c.marking = rocprofiler_configure_external_correlation_id_request_service(
                         c.disp_ctx, kinds, 1, external_corr_request, nullptr) == ROCPROFILER_STATUS_SUCCESS;
-    }
-    if (const char* m = std::getenv("NVRX_CAPTURE_DELIVERY")) {
-        const std::string v(m);
-        if (v == "buffer") {
-            c.delivery = 0;
-        } else if (v == "callback") {
-            c.delivery = 1;
-        } else if (v == "callback_counted") {
-            c.delivery = 2;
-        } else {
-            std::fprintf(stderr, "nvrx capture: NVRX_CAPTURE_DELIVERY=%s is not buffer | callback | "
-                                 "callback_counted; using callback\n", m);
-        }
     }
     if (c.delivery != 0) {
         const rocprofiler_tracing_operation_t complete_only[] = {ROCPROFILER_KERNEL_DISPATCH_COMPLETE};
@@ -403,10 +635,32 @@ void tool_fini(void*) {
     c.ready = false;
 }
 
+// NVRX_CAPTURE_DELIVERY: buffer | callback | callback_counted | queue (anything else: a warning and
+// the default)
+int parse_delivery() {
+    const char* m = std::getenv("NVRX_CAPTURE_DELIVERY");
+    if (!m || !*m) return 1;
+    const std::string v(m);
+    if (v == "buffer") return 0;
+    if (v == "callback") return 1;
+    if (v == "callback_counted") return 2;
+    if (v == "queue") return 3;
+    std::fprintf(stderr, "nvrx capture: NVRX_CAPTURE_DELIVERY=%s is not buffer | callback | "
+                         "callback_counted | queue; using callback\n", m);
+    return 1;
+}
+
 rocprofiler_tool_configure_result_t* nvrx_tool_configure(uint32_t, const char*, uint32_t,
                                                          rocprofiler_client_id_t* id) {
     id->name = "nvrx-straggler";
     cap().client = id;
+    cap().delivery = parse_delivery();
+    if (cap().delivery == 3 &&
+        rocprofiler_at_intercept_table_registration(hsa_table_cb, ROCPROFILER_HSA_TABLE, nullptr) !=
+            ROCPROFILER_STATUS_SUCCESS) {
+        std::fprintf(stderr, "nvrx capture: the HSA intercept table is not available; using callback delivery\n");
+        cap().delivery = 1;
+    }
     static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t),
                                                    &tool_init, &tool_fini, nullptr};
     return &cfg;
@@ -484,13 +738,6 @@ bool wait_uncounted(Capture& c) {
     return true;
 }
 
-// the calling thread's marking (capture_self_begin / _end nest on one thread)
-struct SelfMark {
-    int depth = 0;
-    int slot = -1;
-};
-thread_local SelfMark t_mark;
-
 }  // namespace
 
 namespace nvrx {
@@ -501,6 +748,10 @@ int capture_start(nvrx_profiler* p) {
     Capture& c = cap();
     if (!c.ready) return 0;
     c.target.store(p);
+    if (c.delivery == 3) {
+        c.qactive.store(true, std::memory_order_release);
+        return 0;
+    }
     return rocprofiler_start_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
 }
 
@@ -510,11 +761,19 @@ int capture_stop(nvrx_profiler* p) {
     // no flush here: records of kernels enqueued while started are delivered later and still
     // counted, as CUPTI's are (their completions still arrive with the context stopped)
     (void)p;
+    if (c.delivery == 3) {
+        c.qactive.store(false, std::memory_order_release);
+        return 0;
+    }
     return rocprofiler_stop_context(c.disp_ctx) == ROCPROFILER_STATUS_SUCCESS ? 0 : -1;
 }
 
 void capture_drain(nvrx_profiler* p) {
     Capture& c = cap();
+    if (c.delivery == 3) {  // what has completed, on this thread
+        q_harvest(p);
+        return;
+    }
     if (c.delivery == 0 || !p) return;
     thread_local std::vector<nvrx::DispatchRec> batch;
     batch.clear();
@@ -535,7 +794,10 @@ int capture_flush() {
     } drain;
     const auto t0 = std::chrono::steady_clock::now();
     c.flush_t0.store(t0.time_since_epoch().count());
-    const bool ok = c.marking ? wait_owed(c) : wait_uncounted(c);
+    // queue delivery: nothing to wait for -- the harvest (Drain) takes every dispatch whose
+    // completion signal the device has written, and only those
+    const bool ok = c.delivery == 3 ? (c.n_counted_flush.fetch_add(1), true)
+                                    : c.marking ? wait_owed(c) : wait_uncounted(c);
     const auto t1 = std::chrono::steady_clock::now();
     const int64_t last = c.last_cb_end.load();
     if (last >= c.flush_t0.load()) c.flush_tail_ns.fetch_add((uint64_t)(t1.time_since_epoch().count() - last));
@@ -551,6 +813,10 @@ int capture_flush() {
 // (the caller then pauses the dispatch context instead).
 bool capture_self_begin() {
     Capture& c = cap();
+    if (c.ready && c.delivery == 3) {  // the intercept handler reads the depth on the launching thread
+        ++t_mark.depth;
+        return true;
+    }
     if (!c.ready || !c.marking) return false;
     if (t_mark.depth > 0) {
         ++t_mark.depth;
@@ -570,7 +836,7 @@ bool capture_self_begin() {
 }
 
 void capture_self_end() {
-    if (t_mark.depth == 0 || --t_mark.depth > 0) return;
+    if (t_mark.depth == 0 || --t_mark.depth > 0 || t_mark.slot < 0) return;
     Capture& c = cap();
     c.marks[t_mark.slot].store(0, std::memory_order_release);
     c.n_marked.fetch_sub(1, std::memory_order_release);
@@ -582,8 +848,12 @@ void capture_detach(nvrx_profiler* p) {
     if (c.target.load() != p) return;
     if (c.ready) (void)capture_flush();  // deliver what is pending, to p
     nvrx_profiler* cur = p;
-    if (c.target.compare_exchange_strong(cur, nullptr) && c.ready)
-        (void)rocprofiler_stop_context(c.disp_ctx);
+    if (c.target.compare_exchange_strong(cur, nullptr) && c.ready) {
+        if (c.delivery == 3)
+            c.qactive.store(false, std::memory_order_release);
+        else
+            (void)rocprofiler_stop_context(c.disp_ctx);
+    }
     while (c.inflight.load() != 0) std::this_thread::yield();  // callbacks that loaded p
     capture_drain(p);  // what those callbacks queued is p's, not the next profiler's
 }
@@ -606,7 +876,10 @@ int nvrx_capture_configure(void) {
     return NVRX_OK;
 }
 
-int nvrx_profiler_capture_available(void) { return cap().ready.load() ? 1 : 0; }
+int nvrx_profiler_capture_available(void) {
+    const Capture& c = cap();
+    return c.ready.load() && (c.delivery != 3 || c.q_installed.load()) ? 1 : 0;
+}
 
 int nvrx_capture_stats(nvrx_capture_counters* out) {
     if (!out) {

@@ -79,17 +79,23 @@ def _busy(n):
     return [subprocess.Popen([sys.executable, "-c", "while True: pass"]) for _ in range(n)]
 
 
-def test_flush_is_complete_under_host_load():
+DELIVERY = {"callback": 1, "queue": 3}
+
+
+@pytest.mark.parametrize("delivery", sorted(DELIVERY))
+def test_flush_is_complete_under_host_load(delivery):
     ncpu = len(os.sched_getaffinity(0))
     hogs = _busy(min(32, 2 * ncpu))
     try:
-        out = _child(LOADED)
+        out = _child(LOADED, env={"NVRX_CAPTURE_DELIVERY": delivery})
     finally:
         for h in hogs:
             h.kill()
         for h in hogs:
             h.wait()
-    assert out["delivery"] == 1 and out["marking"] == 1, out  # the shipped default
+    assert out["delivery"] == DELIVERY[delivery], out
+    if delivery == "callback":  # counted through the external-correlation-id request
+        assert out["marking"] == 1, out
     for i, (g, w) in enumerate(zip(out["got"], out["want"])):
         assert g == w, (i, g, w)  # exact per interval: none lost, none carried over
     assert out["counted"] >= 8 and out["quiet"] == 0, out
