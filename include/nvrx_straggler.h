@@ -346,6 +346,11 @@ typedef struct nvrx_capture_counters {
      * request service is on. */
     int64_t enqueues_counted, counted_flushes, quiet_flushes, flush_timeouts, owed_abandoned;
     int32_t delivery, marking;
+    /* queue delivery (3): HSA queues intercepted, dispatches given a completion record of the
+     * device ring, dispatches given a pooled HSA signal instead (ring full or absent), packets
+     * whose own completion signal was chained behind them, and ring records found past their
+     * expected value (0 unless the packet processor does not decrement by one) */
+    int64_t queues, ring_records, pool_signals, chained_signals, ring_anomalies;
 } nvrx_capture_counters;
 int nvrx_capture_stats(nvrx_capture_counters* out);
 

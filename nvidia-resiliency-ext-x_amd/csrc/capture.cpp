@@ -1,43 +1,55 @@
-// capture.cpp -- live kernel-dispatch capture through rocprofiler-sdk (replaces the CUPTI
-// activity path of nvrx_cupti_module: CuptiProfiler.cpp:96-203).
+// capture.cpp -- live kernel-dispatch capture (replaces the CUPTI activity path of
+// nvrx_cupti_module: CuptiProfiler.cpp:96-203).
 //
 // The reference enables CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL, receives activity buffers on
 // CUPTI's thread and, per record, builds the key "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled
 // kernel name, block dims, grid dims in blocks) and pushes (end - start) / 1000.0f into that
-// key's ring.  Here a rocprofiler-sdk tool owns two contexts:
-//   * "symbols"  (started at configuration): code-object callback tracing, kernel_id -> name;
-//   * "dispatch" (started / stopped with the profiler handle): KERNEL_DISPATCH callback tracing
-//     (the default; NVRX_CAPTURE_DELIVERY=buffer selects buffer tracing instead), plus the
+// key's ring.  Here a rocprofiler-sdk tool owns a "symbols" context (code-object callback tracing,
+// kernel_id / kernel_object -> name, started at configuration) and one of two capture mechanisms:
+//   * queue delivery (the default, "Queue delivery" below): through rocprofiler-sdk's
+//     intercept-table service the library takes hsa_queue_create, so every HSA queue the HIP runtime
+//     creates is an intercept queue; while the profiler is started each kernel dispatch packet gets
+//     a completion record in device memory, whose start / end timestamps the packet processor
+//     writes, and flushes harvest the records that completed -- nothing runs per dispatch but a
+//     packet copy, nothing per completion at all (GPT-2 small, profiling_interval 1: +0.7 % per
+//     training step, profiles/r05/capture_queue.json);
+//   * the rocprofiler-sdk KERNEL_DISPATCH modes (NVRX_CAPTURE_DELIVERY=callback | buffer |
+//     callback_counted): a "dispatch" context with callback (or buffer) tracing, plus the
 //     external-correlation-id request service that marks the library's own report kernels and
-//     counts every job dispatch at enqueue (below).
+//     counts every job dispatch at enqueue ("Flush completeness" below) -- ~5 us of
+//     rocprofiler-sdk work per dispatch, +10 % per GPT-2 step.
 // Each completed dispatch becomes the reference's key (workgroup size = block dims; grid_size is
 // in work-items, so blocks = ceil(grid_size / workgroup_size)) and an integer-ns duration record
-// queued for the profiler handle; the per-key rings and statistics are then the HIP kernels of
-// the report path.
+// for the profiler handle; the per-key rings and statistics are then the HIP kernels of the report
+// path.
 //
-// Flush completeness.  The reference's getStats calls cuptiActivityFlushAll(0) after the
-// Detector's torch.cuda.synchronize() (CuptiProfiler.cpp:138, straggler.py:234-235): every kernel
-// that completed is in the report.  rocprofiler-sdk hands a completion over on the runtime's
-// signal-handler thread, some time after the device finished -- long after it when the host is
-// loaded.  So every job dispatch is counted at enqueue, in the external-correlation-id request
-// rocprofiler-sdk makes on the launching thread (a callback that is on anyway for the marking, so
-// the count is one atomic add), under the current flush EPOCH, which the request hands back as
-// the dispatch's external correlation id.  Its completion subtracts it from that epoch once the
-// record is queued.  A flush opens a new epoch and waits until no earlier epoch is owed anything:
-// every dispatch enqueued before the flush has then been handed over, however late the runtime's
-// thread ran.  A dispatch that is still running (enqueued by another thread after the caller's
-// synchronize) is waited for up to NVRX_CAPTURE_FLUSH_TIMEOUT_MS (default 1000); then its epoch
-// is given up, counted (flush_timeouts, owed_abandoned), and the record joins a later report.
+// Flush completeness (rocprofiler-sdk modes).  The reference's getStats calls
+// cuptiActivityFlushAll(0) after the Detector's torch.cuda.synchronize() (CuptiProfiler.cpp:138,
+// straggler.py:234-235): every kernel that completed is in the report.  rocprofiler-sdk hands a
+// completion over on the runtime's signal-handler thread, some time after the device finished --
+// long after it when the host is loaded.  So every job dispatch is counted at enqueue, in the
+// external-correlation-id request rocprofiler-sdk makes on the launching thread (a callback that is
+// on anyway for the marking, so the count is one atomic add), under the current flush EPOCH, which
+// the request hands back as the dispatch's external correlation id.  Its completion subtracts it
+// from that epoch once the record is queued.  A flush opens a new epoch and waits until no earlier
+// epoch is owed anything: every dispatch enqueued before the flush has then been handed over,
+// however late the runtime's thread ran.  A dispatch that is still running (enqueued by another
+// thread after the caller's synchronize) is waited for up to NVRX_CAPTURE_FLUSH_TIMEOUT_MS (default
+// 1000); then its epoch is given up, counted (flush_timeouts, owed_abandoned), and the record joins
+// a later report.  (Queue delivery needs none of this: a flush reads the completion records
+// themselves, which the device writes before the kernel counts as complete.)
 //
 // rocprofiler-sdk tools configure when the ROCm runtime initialises: nvrx_capture_configure
 // must run before the process's first HIP call (the Python side does it at
 // KernelProfiler(capture=True) construction and reports whether it took effect).
+#include <hip/hip_runtime.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 // the installed hsa_api_trace.h names its sibling headers "inc/..." unless built as part of the runtime
 #define AMD_INTERNAL_BUILD
 #include <hsa/hsa_api_trace.h>
 #undef AMD_INTERNAL_BUILD
+#include <hsa/amd_hsa_signal.h>
 #include <rocprofiler-sdk/external_correlation.h>
 #include <rocprofiler-sdk/intercept_table.h>
 #include <rocprofiler-sdk/registration.h>
@@ -80,12 +92,14 @@ struct Capture {
     // the time from the end of its last callback to its return
     std::atomic<int64_t> flush_t0{0}, last_cb_end{0};
     std::atomic<uint64_t> flush_first_cb_ns{0}, flush_cbs{0}, flush_tail_ns{0};
-    // delivery (NVRX_CAPTURE_DELIVERY): 0 = buffer (records batched by rocprofiler-sdk; a flush
-    // also flushes the buffer, ~3.4-5 ms whenever records are pending), 1 = callback, the
-    // default (each completed dispatch handed over as the runtime processes its completion),
-    // 2 = callback_counted (1 + ENQUEUE callbacks on the launching thread, which count the
-    // dispatches when the marking service below is off; kept for cost attribution).
-    int delivery = 1;
+    // delivery (NVRX_CAPTURE_DELIVERY): 3 = queue, the default (HSA intercept queues and device
+    // completion records, no rocprofiler-sdk dispatch tracing; "Queue delivery" below); the
+    // rocprofiler-sdk KERNEL_DISPATCH modes: 1 = callback (each completed dispatch handed over as
+    // the runtime processes its completion), 0 = buffer (records batched by rocprofiler-sdk; a
+    // flush also flushes the buffer, ~3.4-5 ms whenever records are pending), 2 = callback_counted
+    // (1 + ENQUEUE callbacks on the launching thread, which count the dispatches when the marking
+    // service below is off; kept for cost attribution).
+    int delivery = 3;
     std::atomic<uint64_t> n_enqueued{0}, n_completed{0};
     // callback delivery runs on the runtime's completion (signal-handler) thread, which must never
     // wait for the profiler's lock: the caller's thread may hold it across a HIP call that needs
@@ -114,10 +128,13 @@ struct Capture {
     // intercepted queue gets a completion signal of ours while started; pending = dispatches not
     // harvested yet (enqueue order), pool = free signals (value 1); both under pmu
     struct Pending {
-        hsa_signal_t sig;
-        hsa_agent_t agent;
-        uint64_t obj;  // kernel_object of the packet
+        hsa_signal_t sig;   // a pool signal, or the address of a ring record (slot >= 0)
+        const void* queue;  // its QueueInfo
+        uint64_t obj;       // kernel_object of the packet
         uint32_t bx, by, bz, gx, gy, gz;
+        int64_t slot;       // ring slot, -1: pool signal
+        uint64_t seq;       // ring hand-out number (slot = seq % ring_n)
+        int64_t want;       // the ring record's value once this dispatch has completed
     };
     std::mutex pmu;
     std::vector<Pending> pending;
@@ -126,6 +143,25 @@ struct Capture {
     std::atomic<bool> q_installed{false}; // hsa_queue_create is ours
     std::atomic<uint64_t> n_queues{0}, n_signals{0}, n_signal_fail{0}, n_chained{0};
     double tick_ns = 0.0;                 // ns per HSA system timestamp tick (first harvest)
+    // NVRX_CAPTURE_QUEUE_DIAG (cost attribution only; outputs wrong): 1 = intercept, no signals;
+    // 2 = signals on queues without profiling (no timestamps)
+    int qdiag = 0;
+    // raw timestamps: the CP's start_ts / end_ts read from the signal itself (amd_signal_t) in GPU
+    // ticks, checked against hsa_amd_profiling_get_dispatch_time on the first harvest (-1: not yet)
+    int raw_ok = -1;
+    // the ring of completion records in device memory (queue delivery, "Completion records" below):
+    // ring_val = the value each record holds once its last hand-out has completed (host, pmu)
+    amd_signal_t* ring = nullptr;
+    int64_t ring_n = 0;
+    int64_t ring_pci = -2;  // the ring's device (QueueInfo::pci): only its queues take ring records
+    std::vector<int64_t> ring_val;
+    std::vector<uint8_t> ring_busy;
+    uint64_t ring_next = 0;
+    amd_signal_t* ring_host = nullptr;  // pinned mirror the harvest copies into
+    hipStream_t ring_stream = nullptr;
+    bool ring_tried = false;
+    std::mutex ring_copy_mu;            // one harvest copy at a time
+    std::atomic<uint64_t> n_ring{0}, n_ring_full{0}, n_ring_bad{0};
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -140,6 +176,8 @@ struct SelfMark {
     int slot = -1;
 };
 thread_local SelfMark t_mark;
+
+int64_t env_int(const char* name, int64_t dflt);  // an integer environment setting (below)
 
 void code_object_cb(rocprofiler_callback_tracing_record_t record, rocprofiler_user_data_t*,
                     void*) {
@@ -350,17 +388,18 @@ void dispatch_callback_cb(rocprofiler_callback_tracing_record_t record, rocprofi
 }
 
 // ------------------------------------------------------------------------------- queue delivery
-// NVRX_CAPTURE_DELIVERY=queue: no rocprofiler-sdk dispatch tracing at all.  Through
+// NVRX_CAPTURE_DELIVERY=queue (the default): no rocprofiler-sdk dispatch tracing at all.  Through
 // rocprofiler-sdk's intercept-table service the library takes hsa_queue_create: every queue the
 // HIP runtime creates is an HSA intercept queue with profiling enabled, and while the profiler is
 // started each kernel dispatch packet (on a thread that is not running a report of ours) gets a
-// completion signal from a pool -- the CP then writes the kernel's start / end timestamps into it.
-// Nothing runs per completion: a flush (and stop) harvests, in enqueue order, every pending
-// dispatch whose signal has reached 0 -- exactly the kernels that completed, as
-// cuptiActivityFlushAll(0) delivers them (CuptiProfiler.cpp:138) -- reads its timestamps
-// (hsa_amd_profiling_get_dispatch_time) and returns the signal to the pool.  A packet that
-// carried a completion signal of its own keeps it through a barrier-AND packet right behind it
-// (barrier bit set: it completes once the kernel has, and signals the original).
+// completion record -- a record of the device ring ("Completion records" below), or a pooled HSA
+// signal when the ring is full or the queue belongs to another device -- into which the packet
+// processor writes the kernel's start / end timestamps and then decrements it.  Nothing runs per
+// completion: a flush (and stop) harvests, in enqueue order, every pending dispatch whose record
+// shows it completed -- exactly the kernels that completed, as cuptiActivityFlushAll(0) delivers
+// them (CuptiProfiler.cpp:138) -- and frees the record.  A packet that carried a completion signal
+// of its own keeps it through a barrier-AND packet right behind it (barrier bit set: it completes
+// once the kernel has, and signals the original).
 struct QueueFns {
     decltype(hsa_queue_create)* queue_create = nullptr;
     decltype(hsa_amd_queue_intercept_create)* icreate = nullptr;
@@ -371,11 +410,14 @@ struct QueueFns {
     decltype(hsa_signal_load_scacquire)* load = nullptr;
     decltype(hsa_signal_store_relaxed)* store = nullptr;
     decltype(hsa_system_get_info)* sys_info = nullptr;
+    decltype(hsa_agent_get_info)* agent_info = nullptr;
 };
 QueueFns qf;
 
 struct QueueInfo {
     hsa_agent_t agent;
+    double ns_per_tick;  // the agent's timestamp counter (HSA_AMD_AGENT_INFO_TIMESTAMP_FREQUENCY)
+    int64_t pci;         // (PCI domain, bus, device) of the agent; -1 unknown
 };
 
 constexpr uint16_t packet_type(uint16_t header) {
@@ -399,7 +441,11 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
         writer(pkts, n);
         return;
     }
-    const hsa_agent_t agent = static_cast<const QueueInfo*>(data)->agent;
+    if (c.qdiag == 1) {  // diagnostic: the interception alone
+        c.n_requested.fetch_add(nk, std::memory_order_relaxed);
+        writer(pkts, n);
+        return;
+    }
     thread_local std::vector<hsa_signal_t> sigs;
     sigs.assign(nk, hsa_signal_t{0});
     {
@@ -407,20 +453,42 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
         uint64_t j = 0;
         for (uint64_t i = 0; i < n; ++i) {
             if (packet_type(in[i].header) != HSA_PACKET_TYPE_KERNEL_DISPATCH) continue;
-            if (c.pool.empty()) {  // grow (rare: the pool keeps what reports returned)
-                for (int g = 0; g < 256; ++g) {
-                    hsa_signal_t s{0};
-                    if (qf.signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &s) != HSA_STATUS_SUCCESS) break;
-                    c.pool.push_back(s);
-                }
-                if (c.pool.empty()) break;
-            }
-            const hsa_signal_t s = c.pool.back();
-            c.pool.pop_back();
-            sigs[j++] = s;
             const hsa_kernel_dispatch_packet_t& k = in[i];
-            c.pending.push_back({s, agent, k.kernel_object, k.workgroup_size_x, k.workgroup_size_y,
-                                 k.workgroup_size_z, k.grid_size_x, k.grid_size_y, k.grid_size_z});
+            Capture::Pending e{hsa_signal_t{0}, data, k.kernel_object, k.workgroup_size_x, k.workgroup_size_y,
+                               k.workgroup_size_z, k.grid_size_x, k.grid_size_y, k.grid_size_z, -1, 0, 0};
+            // a free record of the ring (a busy one -- a kernel still unharvested -- is skipped), for
+            // a queue of the ring's own device (another GPU's packet processor may not map it)
+            if (c.ring && static_cast<const QueueInfo*>(data)->pci == c.ring_pci) {
+                for (int tries = 0; tries < 8 && e.slot < 0; ++tries) {
+                    const uint64_t seq = c.ring_next++;
+                    const int64_t s = (int64_t)(seq % (uint64_t)c.ring_n);
+                    if (c.ring_busy[s]) continue;
+                    c.ring_busy[s] = 1;
+                    e.slot = s;
+                    e.seq = seq;
+                    e.want = --c.ring_val[s];
+                    e.sig.handle = (uint64_t)(uintptr_t)(c.ring + s);
+                }
+                if (e.slot < 0) c.n_ring_full.fetch_add(1, std::memory_order_relaxed);
+                else c.n_ring.fetch_add(1, std::memory_order_relaxed);
+            }
+            if (e.slot < 0) {  // an HSA signal of the pool
+                if (c.pool.empty()) {  // grow (rare: the pool keeps what reports returned)
+                    for (int g = 0; g < 256; ++g) {
+                        hsa_signal_t s{0};
+                        if (qf.signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &s) != HSA_STATUS_SUCCESS) break;
+                        c.pool.push_back(s);
+                    }
+                }
+                if (c.pool.empty()) {
+                    ++j;  // no signal: the packet goes out as it came
+                    continue;
+                }
+                e.sig = c.pool.back();
+                c.pool.pop_back();
+            }
+            sigs[j++] = e.sig;
+            c.pending.push_back(e);
         }
     }
     thread_local std::vector<hsa_kernel_dispatch_packet_t> out;  // 64-byte AQL slots
@@ -455,7 +523,9 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
             c.n_chained.fetch_add(1, std::memory_order_relaxed);
         }
     }
-    c.n_signals.fetch_add(nk, std::memory_order_relaxed);
+    uint64_t attached = 0;
+    for (const auto& s : sigs) attached += s.handle != 0;
+    c.n_signals.fetch_add(attached, std::memory_order_relaxed);
     c.n_requested.fetch_add(nk, std::memory_order_relaxed);
     writer(out.data(), out.size());
 }
@@ -468,9 +538,15 @@ hsa_status_t q_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
     if (st != HSA_STATUS_SUCCESS)  // not interceptable: a plain queue, not captured
         return qf.queue_create(agent, size, type, callback, data, private_segment_size, group_segment_size,
                                queue);
-    auto* qi = new QueueInfo{agent};  // queues live as long as the process: a few bytes each
+    uint64_t freq = 0;
+    (void)qf.agent_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_TIMESTAMP_FREQUENCY, &freq);
+    uint32_t bdf = 0, dom = 0;
+    const bool pci_ok = qf.agent_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
+                        qf.agent_info(agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS;
+    auto* qi = new QueueInfo{agent, freq ? 1e9 / (double)freq : 0.0,  // queues live as long as the process
+                             pci_ok ? ((int64_t)dom << 16) | (int64_t)(bdf >> 3) : -1};
     if (qf.iregister(*queue, q_intercept, qi) != HSA_STATUS_SUCCESS ||
-        qf.prof_enable(*queue, 1) != HSA_STATUS_SUCCESS)
+        (cap().qdiag != 2 && qf.prof_enable(*queue, 1) != HSA_STATUS_SUCCESS))
         std::fprintf(stderr, "nvrx capture: could not intercept an HSA queue; its kernels are not captured\n");
     cap().n_queues.fetch_add(1);
     return st;
@@ -490,51 +566,183 @@ void hsa_table_cb(rocprofiler_intercept_table_t type, uint64_t, uint64_t, void**
     qf.load = t->core_->hsa_signal_load_scacquire_fn;
     qf.store = t->core_->hsa_signal_store_relaxed_fn;
     qf.sys_info = t->core_->hsa_system_get_info_fn;
+    qf.agent_info = t->core_->hsa_agent_get_info_fn;
     if (!qf.queue_create || !qf.icreate || !qf.iregister || !qf.prof_enable || !qf.dispatch_time ||
-        !qf.signal_create || !qf.load || !qf.store || !qf.sys_info)
+        !qf.signal_create || !qf.load || !qf.store || !qf.sys_info || !qf.agent_info)
         return;
+    cap().qdiag = (int)env_int("NVRX_CAPTURE_QUEUE_DIAG", 0);
     t->core_->hsa_queue_create_fn = q_create;
     cap().q_installed = true;
 }
 
-// the completed pending dispatches, in enqueue order, into p (or dropped without one); the
-// signals go back to the pool
+// Completion records.  A completion signal in host memory costs every kernel ~1.2 us on the device
+// (the packet processor's atomic on the signal crosses to host memory before the next packet of the
+// queue may start: empty kernels 2.6 -> 4.0 us each, GPT-2 small +4.5 % per step,
+// profiles/r05/capture_queue.json).  So the packets' completion "signals" are amd_signal_t records
+// of a ring in fine-grained device memory (the CP decrements and timestamps them like any signal;
+// no runtime object, no event mailbox, so no interrupt), each record's value counting down from
+// 2^40 over its hand-outs: a dispatch has completed when its record holds the value the host
+// expects after it (Pending::want).  A harvest copies the range of records still pending to a pinned
+// mirror on a stream of its own (never waiting for the job's kernels) and reads them there.
+constexpr int64_t RING_INIT = (int64_t)1 << 40;
+
+void ring_setup() {  // on a caller's thread (HIP calls allowed), before the first hand-out
+    Capture& c = cap();
+    if (c.ring_tried) return;
+    c.ring_tried = true;
+    const int64_t n = env_int("NVRX_CAPTURE_RING", (int64_t)1 << 19);
+    if (n <= 0) return;
+    std::vector<amd_signal_t> h((size_t)n);
+    std::memset(h.data(), 0, h.size() * sizeof(amd_signal_t));
+    for (auto& s : h) {
+        s.kind = AMD_SIGNAL_KIND_USER;
+        s.value = RING_INIT;
+    }
+    int dev = 0, bus = 0, slot = 0, dom = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&slot, hipDeviceAttributePciDeviceId, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, dev) != hipSuccess)
+        return;
+    void* d = nullptr;
+    void* m = nullptr;
+    hipStream_t st = nullptr;
+    const size_t bytes = (size_t)n * sizeof(amd_signal_t);
+    if (hipExtMallocWithFlags(&d, bytes, hipDeviceMallocFinegrained) != hipSuccess ||
+        hipHostMalloc(&m, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+        hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        std::fprintf(stderr, "nvrx capture: no device completion ring (%s); using HSA signals\n",
+                     hipGetErrorString(hipGetLastError()));
+        if (d) (void)hipFree(d);
+        if (m) (void)hipHostFree(m);
+        if (st) (void)hipStreamDestroy(st);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(c.pmu);
+    c.ring_val.assign((size_t)n, RING_INIT);
+    c.ring_busy.assign((size_t)n, 0);
+    c.ring_host = static_cast<amd_signal_t*>(m);
+    c.ring_stream = st;
+    c.ring_n = n;
+    c.ring_pci = ((int64_t)dom << 16) | (int64_t)((bus << 5) | (slot & 31));
+    c.ring = static_cast<amd_signal_t*>(d);
+}
+
+// ring records [seq_lo, seq_hi) -> the pinned mirror (slot-indexed), synchronously on the ring's stream
+bool ring_copy(uint64_t seq_lo, uint64_t seq_hi) {
+    Capture& c = cap();
+    const uint64_t n = (uint64_t)c.ring_n;
+    uint64_t cnt = std::min<uint64_t>(seq_hi - seq_lo, n);
+    uint64_t s = seq_lo % n;
+    hipError_t e = hipSuccess;
+    while (cnt > 0 && e == hipSuccess) {
+        const uint64_t m = std::min<uint64_t>(cnt, n - s);
+        e = hipMemcpyAsync(c.ring_host + s, c.ring + s, m * sizeof(amd_signal_t), hipMemcpyDeviceToHost,
+                           c.ring_stream);
+        cnt -= m;
+        s = 0;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c.ring_stream);
+    return e == hipSuccess;
+}
+
+// the completed pending dispatches, in enqueue order, into p (or dropped without one); pool signals
+// go back to the pool, ring records become free
 void q_harvest(nvrx_profiler* p) {
     Capture& c = cap();
     if (!c.q_installed) return;
     thread_local std::vector<Capture::Pending> done;
     thread_local std::vector<nvrx::DispatchRec> batch;
+    thread_local std::vector<uint64_t> ring_ns;  // durations of the harvested ring records (done order)
     done.clear();
     batch.clear();
+    ring_ns.clear();
+    std::unique_lock<std::mutex> copy_lk(c.ring_copy_mu);  // the mirror is shared
+    // the hand-out range of the ring records pending now
+    bool any_ring = false;
+    uint64_t lo = ~0ull, hi = 0;
+    {
+        std::lock_guard<std::mutex> lk(c.pmu);
+        for (const auto& e : c.pending)
+            if (e.slot >= 0) {
+                any_ring = true;
+                lo = std::min(lo, e.seq);
+                hi = std::max(hi, e.seq + 1);
+            }
+    }
+    const bool copied = any_ring && ring_copy(lo, hi);
     {
         std::lock_guard<std::mutex> lk(c.pmu);
         size_t w = 0;
         for (size_t i = 0; i < c.pending.size(); ++i) {
-            if (qf.load(c.pending[i].sig) == 0)
-                done.push_back(c.pending[i]);
+            const Capture::Pending& e = c.pending[i];
+            bool complete = false;
+            if (e.slot < 0) {
+                complete = qf.load(e.sig) == 0;
+            } else if (copied && e.seq >= lo && e.seq < hi) {
+                const amd_signal_t& r = c.ring_host[e.slot];
+                complete = r.value <= e.want;
+                if (complete) {
+                    if (r.value != e.want) c.n_ring_bad.fetch_add(1, std::memory_order_relaxed);
+                    const double npt = static_cast<const QueueInfo*>(e.queue)->ns_per_tick;
+                    ring_ns.push_back(r.end_ts > r.start_ts && npt > 0.0
+                                          ? (uint64_t)((double)(r.end_ts - r.start_ts) * npt + 0.5) : 0);
+                    c.ring_busy[e.slot] = 0;
+                }
+            }
+            if (complete)
+                done.push_back(e);
             else
-                c.pending[w++] = c.pending[i];
+                c.pending[w++] = e;
         }
         c.pending.resize(w);
     }
+    copy_lk.unlock();
     if (done.empty()) return;
     if (c.tick_ns == 0.0) {
         uint64_t f = 0;
         c.tick_ns = qf.sys_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) == HSA_STATUS_SUCCESS && f
                         ? 1e9 / (double)f : 1.0;
     }
-    uint64_t runtime = 0;
-    for (const auto& e : done) {
+    // pool signals: the duration from the CP's raw timestamps (amd_signal_t, GPU ticks) --
+    // hsa_amd_profiling_get_dispatch_time translates them to the system clock domain, ~0.1 us per
+    // call; the first harvest checks that both give the same duration (to 1 %, >= 1 us)
+    const auto raw_ns = [](const Capture::Pending& e) -> uint64_t {
+        const auto* as = reinterpret_cast<const amd_signal_t*>(e.sig.handle);
+        const double npt = static_cast<const QueueInfo*>(e.queue)->ns_per_tick;
+        return as->end_ts > as->start_ts && npt > 0.0 ? (uint64_t)((double)(as->end_ts - as->start_ts) * npt + 0.5) : 0;
+    };
+    const auto api_ns = [&](const Capture::Pending& e) -> uint64_t {
         hsa_amd_profiling_dispatch_time_t tm{0, 0};
-        (void)qf.dispatch_time(e.agent, e.sig, &tm);
+        (void)qf.dispatch_time(static_cast<const QueueInfo*>(e.queue)->agent, e.sig, &tm);
+        return tm.end > tm.start ? (c.tick_ns == 1.0 ? tm.end - tm.start
+                                                     : (uint64_t)((double)(tm.end - tm.start) * c.tick_ns + 0.5))
+                                 : 0;
+    };
+    if (c.raw_ok < 0) {
+        int agree = 0, total = 0;
+        for (const auto& e : done) {
+            if (e.slot >= 0) continue;
+            const uint64_t a = api_ns(e), r = raw_ns(e);
+            if (a < 1000) continue;
+            ++total;
+            agree += (r > a ? r - a : a - r) * 100 <= a;
+        }
+        if (total > 0) {
+            c.raw_ok = agree == total ? 1 : 0;
+            if (!c.raw_ok)
+                std::fprintf(stderr, "nvrx capture: raw dispatch timestamps disagree with the HSA runtime's "
+                                     "(%d of %d); using hsa_amd_profiling_get_dispatch_time\n", total - agree, total);
+        }
+    }
+    uint64_t runtime = 0;
+    size_t ri = 0;
+    for (const auto& e : done) {
         rocprofiler_kernel_dispatch_info_t di{};
         di.kernel_id = e.obj;
         di.workgroup_size = {e.bx, e.by, e.bz};
         di.grid_size = {e.gx, e.gy, e.gz};
-        const uint64_t ns = tm.end > tm.start
-                                ? (c.tick_ns == 1.0 ? tm.end - tm.start
-                                                    : (uint64_t)((double)(tm.end - tm.start) * c.tick_ns + 0.5))
-                                : 0;
+        const uint64_t ns = e.slot >= 0 ? ring_ns[ri++] : c.raw_ok == 1 ? raw_ns(e) : api_ns(e);
         nvrx::DispatchRec d;
         switch (to_dispatch(di, 0, ns, 0, d)) {
             case Kind::runtime: ++runtime; break;
@@ -545,6 +753,7 @@ void q_harvest(nvrx_profiler* p) {
     {
         std::lock_guard<std::mutex> lk(c.pmu);
         for (const auto& e : done) {
+            if (e.slot >= 0) continue;
             qf.store(e.sig, 1);
             c.pool.push_back(e.sig);
         }
@@ -635,19 +844,19 @@ void tool_fini(void*) {
     c.ready = false;
 }
 
-// NVRX_CAPTURE_DELIVERY: buffer | callback | callback_counted | queue (anything else: a warning and
-// the default)
+// NVRX_CAPTURE_DELIVERY: queue (the default) | callback | callback_counted | buffer (anything else:
+// a warning and the default)
 int parse_delivery() {
     const char* m = std::getenv("NVRX_CAPTURE_DELIVERY");
-    if (!m || !*m) return 1;
+    if (!m || !*m) return 3;
     const std::string v(m);
     if (v == "buffer") return 0;
     if (v == "callback") return 1;
     if (v == "callback_counted") return 2;
     if (v == "queue") return 3;
-    std::fprintf(stderr, "nvrx capture: NVRX_CAPTURE_DELIVERY=%s is not buffer | callback | "
-                         "callback_counted | queue; using callback\n", m);
-    return 1;
+    std::fprintf(stderr, "nvrx capture: NVRX_CAPTURE_DELIVERY=%s is not queue | callback | "
+                         "callback_counted | buffer; using queue\n", m);
+    return 3;
 }
 
 rocprofiler_tool_configure_result_t* nvrx_tool_configure(uint32_t, const char*, uint32_t,
@@ -749,6 +958,7 @@ int capture_start(nvrx_profiler* p) {
     if (!c.ready) return 0;
     c.target.store(p);
     if (c.delivery == 3) {
+        ring_setup();  // once, on the first start (this thread may make HIP calls)
         c.qactive.store(true, std::memory_order_release);
         return 0;
     }
@@ -905,6 +1115,11 @@ int nvrx_capture_stats(nvrx_capture_counters* out) {
     out->owed_abandoned = (int64_t)c.n_abandoned.load();
     out->delivery = c.ready ? c.delivery : -1;
     out->marking = c.marking ? 1 : 0;
+    out->queues = (int64_t)c.n_queues.load();
+    out->ring_records = (int64_t)c.n_ring.load();
+    out->pool_signals = (int64_t)(c.n_signals.load() - c.n_ring.load());
+    out->chained_signals = (int64_t)c.n_chained.load();
+    out->ring_anomalies = (int64_t)c.n_ring_bad.load();
     return NVRX_OK;
 }
 

@@ -62,7 +62,8 @@ class CaptureCounters(ctypes.Structure):
                 ("own_kernels", i64), ("flush_first_cb_ns", i64), ("flush_callbacks", i64),
                 ("flush_tail_ns", i64), ("enqueues_counted", i64), ("counted_flushes", i64),
                 ("quiet_flushes", i64), ("flush_timeouts", i64), ("owed_abandoned", i64),
-                ("delivery", i32), ("marking", i32)]
+                ("delivery", i32), ("marking", i32), ("queues", i64), ("ring_records", i64),
+                ("pool_signals", i64), ("chained_signals", i64), ("ring_anomalies", i64)]
 
 
 class ProfilerConfig(ctypes.Structure):

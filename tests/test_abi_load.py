@@ -62,5 +62,5 @@ def test_capture_counters_without_capture():
     assert (c.callbacks, c.dispatches, c.flushes, c.callback_ns) == (0, 0, 0, 0)
     assert (c.enqueues_counted, c.counted_flushes, c.flush_timeouts, c.delivery) == (0, 0, 0, -1)
     # the C struct and the ctypes mirror agree on the layout (two int32 at the end)
-    assert ctypes.sizeof(c) == 16 * 8 + 2 * 4
+    assert ctypes.sizeof(c) == 16 * 8 + 2 * 4 + 5 * 8
     assert _native.lib().nvrx_capture_stats(None) == _native.NVRX_ERR_INVALID

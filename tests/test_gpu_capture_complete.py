@@ -164,3 +164,45 @@ def test_concurrent_reports_never_capture_own_kernels():
     assert ingested == {f"ext_kernel_{i}": 8192 for i in range(4)}, ingested
     assert set(st) == {job_key} | set(ingested), sorted(st)  # no kernel of the library's own
     assert out["reports"] >= 2 and out["own"] > 0, out
+
+
+DURATIONS = r"""
+import ctypes, json
+from nvidia_resiliency_ext.straggler import cupti, _native
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=1024, capture=True)
+p.initialize()
+torch.cuda._sleep(1000)  # the spin kernel's code object loaded
+torch.cuda.synchronize()
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(40)]
+p.start()
+for a, b in ev:
+    a.record()
+    torch.cuda._sleep(2_000_000)  # ~1 ms of device spin
+    b.record()
+torch.cuda.synchronize()
+st = {k: [v.num_calls, v.median, v.min, v.max] for k, v in p.get_stats().items()}
+c = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c))
+p.stop()
+p.shutdown()
+ms = sorted(a.elapsed_time(b) for a, b in ev)
+print("RESULT " + json.dumps({"stats": st, "event_median_us": ms[len(ms) // 2] * 1e3, "delivery": c.delivery,
+                              "ring": c.ring_records, "pool": c.pool_signals, "anomalies": c.ring_anomalies}))
+"""
+
+
+@pytest.mark.parametrize("delivery", sorted(DELIVERY))
+def test_captured_durations_match_event_timing(delivery):
+    """A ~1 ms device spin launched 40 times between two timing events: the captured duration
+    of each dispatch (the packet processor's timestamps) agrees with the events' elapsed time,
+    which brackets the kernel plus its launch gap, in every delivery mode."""
+    out = _child(DURATIONS, env={"NVRX_CAPTURE_DELIVERY": delivery})
+    assert out["delivery"] == DELIVERY[delivery], out
+    spin = {k: v for k, v in out["stats"].items() if "sleep" in k.lower() or "spin" in k.lower()}
+    assert len(spin) == 1, out["stats"]
+    (num, med, mn, mx), = spin.values()
+    assert num == 40, out
+    ev = out["event_median_us"]
+    assert 0.9 * ev <= med <= 1.01 * ev, (med, ev)
+    if delivery == "queue":  # device completion records, nothing past the expected values
+        assert out["ring"] >= 40 and out["anomalies"] == 0, out
