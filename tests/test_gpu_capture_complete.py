@@ -70,7 +70,9 @@ d = lambda f: getattr(c1, f) - getattr(c0, f)
 print("RESULT " + json.dumps({"got": got, "want": want, "delivery": c1.delivery,
       "marking": c1.marking, "counted": d("counted_flushes"), "quiet": d("quiet_flushes"),
       "timeouts": d("flush_timeouts"), "abandoned": d("owed_abandoned"),
-      "enqueues": d("enqueues_counted"), "flush_ms": d("flush_ns") / 1e6 / max(1, d("flushes"))}))
+      "enqueues": d("enqueues_counted"), "flush_ms": d("flush_ns") / 1e6 / max(1, d("flushes")),
+      "ring": d("ring_records"), "pool": d("pool_signals"), "chained": d("chained_signals"),
+      "anomalies": c1.ring_anomalies}))
 """.replace("STRAG", repr(STRAG))
 
 
@@ -80,14 +82,21 @@ def _busy(n):
 
 
 DELIVERY = {"callback": 1, "queue": 3}
+# queue delivery with a device ring of 64 records: most dispatches of an interval fall back to
+# pooled HSA signals (the ring is full until the next harvest) -- the counts stay exact
+RINGS = {"callback": None, "queue": None, "queue_ring64": "64"}
 
 
-@pytest.mark.parametrize("delivery", sorted(DELIVERY))
-def test_flush_is_complete_under_host_load(delivery):
+@pytest.mark.parametrize("mode", sorted(RINGS))
+def test_flush_is_complete_under_host_load(mode):
+    delivery = mode.split("_")[0]
+    env = {"NVRX_CAPTURE_DELIVERY": delivery}
+    if RINGS[mode]:
+        env["NVRX_CAPTURE_RING"] = RINGS[mode]
     ncpu = len(os.sched_getaffinity(0))
     hogs = _busy(min(32, 2 * ncpu))
     try:
-        out = _child(LOADED, env={"NVRX_CAPTURE_DELIVERY": delivery})
+        out = _child(LOADED, env=env)
     finally:
         for h in hogs:
             h.kill()
@@ -100,6 +109,10 @@ def test_flush_is_complete_under_host_load(delivery):
         assert g == w, (i, g, w)  # exact per interval: none lost, none carried over
     assert out["counted"] >= 8 and out["quiet"] == 0, out
     assert out["timeouts"] == 0 and out["abandoned"] == 0, out
+    if delivery == "queue":
+        launched = sum(sum(w.values()) for w in out["want"])
+        assert out["ring"] + out["pool"] == launched and out["anomalies"] == 0, out
+        assert (out["pool"] > 0) == (mode == "queue_ring64"), out
     # every launch of the 8 intervals was counted at enqueue (the Detector's own kernels run
     # with the profiler stopped, or marked)
     assert out["enqueues"] == sum(sum(w.values()) for w in out["want"]), out
@@ -187,7 +200,8 @@ p.stop()
 p.shutdown()
 ms = sorted(a.elapsed_time(b) for a, b in ev)
 print("RESULT " + json.dumps({"stats": st, "event_median_us": ms[len(ms) // 2] * 1e3, "delivery": c.delivery,
-                              "ring": c.ring_records, "pool": c.pool_signals, "anomalies": c.ring_anomalies}))
+                              "ring": c.ring_records, "pool": c.pool_signals, "anomalies": c.ring_anomalies,
+                              "chained": c.chained_signals}))
 """
 
 
@@ -206,3 +220,75 @@ def test_captured_durations_match_event_timing(delivery):
     assert 0.9 * ev <= med <= 1.01 * ev, (med, ev)
     if delivery == "queue":  # device completion records, nothing past the expected values
         assert out["ring"] >= 40 and out["anomalies"] == 0, out
+
+
+PROBE = os.path.join(ROOT, "tests", "native", "grid_probe.hsaco")
+EXT_EVENTS = r"""
+import ctypes, json
+from nvidia_resiliency_ext.straggler import cupti, _native
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=1024, capture=True)
+p.initialize()
+hip = ctypes.CDLL("libamdhip64.so")
+mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+assert hip.hipModuleLoad(ctypes.byref(mod), PROBE.encode()) == 0
+assert hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"nvrx_spin_alu") == 0
+buf = torch.zeros(64, dtype=torch.float32, device="cuda")
+stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+a_out, a_n = ctypes.c_void_p(buf.data_ptr()), ctypes.c_uint32(400000)
+params = (ctypes.c_void_p * 2)(ctypes.cast(ctypes.byref(a_out), ctypes.c_void_p),
+                               ctypes.cast(ctypes.byref(a_n), ctypes.c_void_p))
+hip.hipExtModuleLaunchKernel.argtypes = [ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [
+    ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+    ctypes.c_void_p, ctypes.c_uint32]
+hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+def launch(ev=None):
+    s, e = ev if ev else (None, None)
+    rc = hip.hipExtModuleLaunchKernel(fn, 64, 1, 1, 64, 1, 1, 0, stream, params, None, s, e, 0)
+    assert rc == 0, rc
+launch()
+torch.cuda.synchronize()
+c0 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c0))
+evs = []
+for _ in range(20):
+    s, e = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipEventCreate(ctypes.byref(s)) == 0 and hip.hipEventCreate(ctypes.byref(e)) == 0
+    evs.append((s, e))
+p.start()
+for ev in evs:
+    launch(ev)  # the runtime times the kernel itself for these events
+for _ in range(20):
+    launch()
+torch.cuda.synchronize()
+st = {k: [v.num_calls, v.median] for k, v in p.get_stats().items()}
+c1 = _native.CaptureCounters(); _native.lib().nvrx_capture_stats(ctypes.byref(c1))
+p.stop()
+p.shutdown()
+ms = []
+for s, e in evs:
+    f = ctypes.c_float()
+    assert hip.hipEventElapsedTime(ctypes.byref(f), s, e) == 0
+    ms.append(f.value)
+ms.sort()
+print("RESULT " + json.dumps({"stats": st, "event_median_us": ms[len(ms) // 2] * 1e3,
+                              "chained": c1.chained_signals - c0.chained_signals, "delivery": c1.delivery}))
+""".replace("PROBE", repr(PROBE))
+
+
+@pytest.mark.parametrize("delivery", sorted(DELIVERY))
+def test_runtime_timed_launches_keep_their_event_timing(delivery):
+    """hipExtModuleLaunchKernel with start / stop events: the runtime times that kernel itself (its
+    own completion signal on the packet, which queue delivery chains behind a completion record of
+    ours).  The events' elapsed time still measures the kernel, and the capture counts all 40
+    launches with the same duration."""
+    assert os.path.exists(PROBE), "build tests/native first (__graft_entry__.build())"
+    out = _child(EXT_EVENTS, env={"NVRX_CAPTURE_DELIVERY": delivery})
+    assert out["delivery"] == DELIVERY[delivery], out
+    spin = {k: v for k, v in out["stats"].items() if k.startswith("nvrx_spin_alu")}
+    assert len(spin) == 1, out["stats"]
+    (num, med), = spin.values()
+    assert num == 40, out
+    ev = out["event_median_us"]
+    assert med > 50 and 0.8 * med <= ev <= 1.3 * med, (med, ev, out["chained"])
+    if delivery == "queue":  # ROCm 7.2 gives exactly the 20 event-timed packets a signal: chained
+        assert out["chained"] == 20, out
