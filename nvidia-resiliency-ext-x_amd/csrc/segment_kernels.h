@@ -80,23 +80,34 @@ enum : int {
     C_T8 = 0, C_T16, C_T32, C_T64, C_T128,    // lane classes
     C_W4, C_W8, C_W16, C_W32, C_W64, C_W128,  // wave classes (PL)
     C_X,                                      // workgroup (EXACT kernel)
+    C_F,                                      // FAST, exactly full_n = 64 * PL samples, 16-B aligned
     NCLASS
 };
 
 // need = retained samples + misalignment slack a wave would have to hold.  Every class is a
 // power-of-two length range, so the class is ceil(log2) of the length, offset: lane classes
 // 1..8 / 9..16 / ... / 65..128, then wave classes of need 129..256 (PL 4) ... 4097..8192 (PL 128).
-__device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact) {
+// full_n (0: none) -- the longest retained length when it is 64 * PL samples for a PL of 16..128
+// and the segments start on 16-B boundaries (FAST): segments of exactly that length, the rings
+// that overflowed (the hot kernels of a live report, configs[3]'s hottest slot), are the FULL
+// class -- no lane masks, and the grouped lane-parallel epilogue (seg_stats_list_full_kernel).
+__device__ __forceinline__ int seg_class(int n, bool aligned16, bool exact, int full_n) {
     if (n <= 128) {
         const int l = 32 - __clz(n - 1);  // ceil(log2 n); 0 for n = 1
         return l <= 3 ? C_T8 : l - 3;     // 4..7 -> C_T16..C_T128
     }
     if (exact) return C_X;
+    if (n == full_n) return C_F;
     const int need = aligned16 ? n : n + 3;
     const int l = 32 - __clz(need - 1);  // 8..13 -> C_W4..C_W128
     return l <= 13 ? l - 3 : C_X;
 }
-static_assert(C_T16 == 1 && C_T128 == 4 && C_W4 == 5 && C_W128 == 10 && C_X == 11, "class order");
+static_assert(C_T16 == 1 && C_T128 == 4 && C_W4 == 5 && C_W128 == 10 && C_X == 11 && C_F == 12,
+              "class order");
+// the FULL length of a launch (seg_class): keep if it is 64 * PL for PL in 16..128, else 0
+inline int full_len(int64_t keep, bool aligned16, bool exact) {
+    return (!exact && aligned16 && (keep == 1024 || keep == 2048 || keep == 4096 || keep == 8192)) ? (int)keep : 0;
+}
 
 // Wave-aggregated class counting: one LDS atomic per distinct class present in the
 // wave (leader = lowest lane); returns this lane's rank among same-class lanes plus the

@@ -144,6 +144,8 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
         if (need > 64 * 16) ragged_launch_list(32, segs, list, c + 2 * C_W32, out, S());
         if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, S());
         if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, S());
+        if (const int fn = full_len(keep, aligned16, exact))  // the FULL class (seg_class)
+            ragged_launch_full(fn / 64, segs, list, c + 2 * C_F, out, S());
     }
     hipError_t e = hipSuccess;
     if (exact ? keep > 128 : need > 64 * 128) e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, S());
@@ -189,11 +191,11 @@ hipError_t segment_stats_ragged(const uint32_t* ns, const int64_t* seg_off, cons
     // against 4.13 for these three launches on configs[3]: the reservations contend on one
     // address per class)
     hipLaunchKernelGGL(classify_count_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st, segs,
-                       nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, out);
+                       nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, full_len(keep, aligned16, exact), bcnt, out);
     hipLaunchKernelGGL(classify_scan_kernel, dim3(1), dim3(CLS_MAX_BLOCKS), 0, st, bcnt, (int)nblocks,
                        cls);
     hipLaunchKernelGGL(classify_scatter_kernel, dim3((unsigned)nblocks), dim3(CLS_THREADS), 0, st,
-                       segs, nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, bcnt, list);
+                       segs, nseg, chunk, aligned16 ? 1 : 0, exact ? 1 : 0, full_len(keep, aligned16, exact), bcnt, list);
     const hipError_t e = ragged_launch_classes(segs, list, cls, keep, aligned16, exact, out, st);
     const hipError_t f = hipFreeAsync(ws, st);  // on the error path too
     if (e != hipSuccess) return e;

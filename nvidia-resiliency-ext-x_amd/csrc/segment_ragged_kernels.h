@@ -12,6 +12,8 @@ namespace nvrx {
 namespace ragged {
 namespace {  // internal linkage: every translation unit keeps its own copy
 
+int cu_count();  // CUs of the current device (below)
+
 
 constexpr int CLS_THREADS = 1024;
 constexpr int CLS_MAX_BLOCKS = 1024;
@@ -22,12 +24,12 @@ constexpr int CLS_MAX_BLOCKS = 1024;
 #define NVRX_CLS_BATCH 8
 #endif
 constexpr int CLS_BATCH = NVRX_CLS_BATCH;
-static_assert(CLS_BATCH >= 1 && CLS_BATCH < 32 && 5 * NCLASS <= 64, "5-bit packed class counts per batch");
+static_assert(CLS_BATCH >= 1 && CLS_BATCH < 16 && 4 * NCLASS <= 64, "4-bit packed class counts per batch");
 
 
 // pass 1: per-block class counts (bcnt[b][c]); empty segments are written here
 __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
-    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, uint32_t* bcnt,
+    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, int full_n, uint32_t* bcnt,
     nvrx_stats_soa out) {
     const ColRef cr{nullptr, nullptr, 1, 1.0};  // column references: kernel_ref afterwards
     __shared__ uint32_t lcnt[NCLASS];
@@ -47,7 +49,7 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
             const int64_t s = b + j * CLS_THREADS + threadIdx.x;
             n[j] = s < hi ? segs.kept_len(s) : -1;
         }
-        // the batch's class counts packed 5 bits per class in one 64-bit word (one shift and
+        // the batch's class counts packed 4 bits per class in one 64-bit word (one shift and
         // add per segment instead of a compare and add per class), unpacked once per batch
         uint64_t pk = 0;
 #pragma unroll
@@ -57,11 +59,11 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_count_kernel(
                 write_empty(out, s);
                 cr.miss(s);
             } else if (n[j] > 0) {  // n < 0: reduced elsewhere (or past the chunk)
-                pk += 1ull << (5 * seg_class(n[j], aligned16 != 0, exact != 0));
+                pk += 1ull << (4 * seg_class(n[j], aligned16 != 0, exact != 0, full_n));
             }
         }
 #pragma unroll
-        for (int c = 0; c < NCLASS; ++c) mine[c] += (uint32_t)(pk >> (5 * c)) & 31u;
+        for (int c = 0; c < NCLASS; ++c) mine[c] += (uint32_t)(pk >> (4 * c)) & 15u;
     }
 #pragma unroll
     for (int c = 0; c < NCLASS; ++c) {
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(CLS_MAX_BLOCKS) void classify_scan_kernel(uint32_t*
 
 // pass 3: scatter segment ids into the class-ordered list
 __global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
-    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, const uint32_t* boff,
+    RaggedSegs segs, int64_t nseg, int64_t chunk, int aligned16, int exact, int full_n, const uint32_t* boff,
     uint32_t* list) {
     __shared__ uint32_t lcnt[NCLASS];
     __shared__ uint32_t lbase[NCLASS];
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(CLS_THREADS) void classify_scatter_kernel(
 #pragma unroll
         for (int j = 0; j < CLS_BATCH; ++j) {  // the same order as the counting pass
             const int64_t s = b + j * CLS_THREADS + threadIdx.x;
-            const int cls = n[j] > 0 ? seg_class(n[j], aligned16 != 0, exact != 0) : -1;
+            const int cls = n[j] > 0 ? seg_class(n[j], aligned16 != 0, exact != 0, full_n) : -1;
             const uint32_t r = wave_class_add(lcnt, cls);
             if (cls >= 0) list[lbase[cls] + r] = (uint32_t)s;
         }
@@ -343,6 +345,78 @@ void seg_stats_list_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t
     }
 }
 
+// FULL classes (seg_class C_F16..C_F128: exactly 64 * PL samples, 16-B aligned, FAST): the
+// configs[1] group kernel's body over a class list -- each wave takes LIST_FULL_GROUP consecutive
+// list entries, lanes 0..m-1 fetch their ids in one access, every segment runs the unmasked
+// lean_core, and segment j's results wait in lane j for one lane-parallel epilogue.
+#ifndef NVRX_LIST_FULL_GROUP  // build-time tuning constant
+#define NVRX_LIST_FULL_GROUP 4
+#endif
+template <int PL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
+void seg_stats_list_full_kernel(RaggedSegs segs, const uint32_t* list, const uint32_t* cls,
+                                nvrx_stats_soa out) {
+    const ColRef cr{nullptr, nullptr, 1, 1.0};  // column references: kernel_ref afterwards
+    constexpr int NB = Bins<PL>::NB;
+    constexpr uint32_t G = NVRX_LIST_FULL_GROUP;
+    __shared__ __attribute__((aligned(16))) unsigned lds_hist[4 * NB];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = lane_id();
+    unsigned* hist = lds_hist + wave * NB;
+    const uint32_t start = cls[0], cnt = cls[1];
+    const uint32_t W = gridDim.x * 4u;
+    for (uint32_t c0 = (blockIdx.x * 4u + wave) * G; c0 < cnt; c0 += W * G) {
+        const int m = (int)min(G, cnt - c0);
+        const uint32_t sid = lane < m ? list[start + c0 + lane] : 0u;
+        unsigned a_mn = 0, a_mx = 0, a_k0 = 0, a_k1 = 0, a_c = 0, a_sdlo = 0, a_sdhi = 0, a_sqlo = 0,
+                 a_sqhi = 0;
+        uint32_t wide = 0;
+        int n = 0;
+        for (int j = 0; j < m; ++j) {
+            const int64_t s = (uint32_t)__builtin_amdgcn_readlane((int)sid, j);
+            const uint32_t* p;
+            segs.get(s, p, n);  // n == 64 * PL (the class)
+            unsigned v[PL];
+            int m0;
+            unsigned x0;
+            load_segment<PL, true>(p, n, v, m0, x0);
+            const LeanOut<PL> r = lean_core<PL>(v, n, 0, x0, hist);
+            const uint64_t sqb = (uint64_t)__double_as_longlong(r.sq);
+            const uint64_t sdb = sd_bits(r.sd);
+            const bool mine = lane == j;
+            a_mn = mine ? r.mn : a_mn;
+            a_mx = mine ? r.mx : a_mx;
+            a_k0 = mine ? r.mn + r.d0 : a_k0;
+            a_k1 = mine ? r.mn + r.d1 : a_k1;
+            a_c = mine ? r.c : a_c;
+            a_sdlo = mine ? (uint32_t)sdb : a_sdlo;
+            a_sdhi = mine ? (uint32_t)(sdb >> 32) : a_sdhi;
+            a_sqlo = mine ? (uint32_t)sqb : a_sqlo;
+            a_sqhi = mine ? (uint32_t)(sqb >> 32) : a_sqhi;
+            if (r.mx >= NVRX_KEY_WIDE) wide |= 1u << j;
+        }
+        if (lane < m)
+            emit_lane(out, (int64_t)sid, n, a_mn, a_mx, a_k0, a_k1,
+                      sd_value<PL>(((uint64_t)a_sdhi << 32) | a_sdlo),
+                      __longlong_as_double((long long)(((uint64_t)a_sqhi << 32) | a_sqlo)), a_c, cr);
+        while (wide) {  // keys of >= 3.76 s: the decoded moments (rare)
+            const int j = __builtin_ffs(wide) - 1;
+            wide &= wide - 1;
+            const int64_t s = (uint32_t)__builtin_amdgcn_readlane((int)sid, j);
+            const uint32_t* p;
+            segs.get(s, p, n);
+            wide_moments(p, n, s, out);
+        }
+    }
+}
+
+template <int PL>
+void launch_list_full(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                      const nvrx_stats_soa& out, hipStream_t st) {
+    const unsigned blocks = (unsigned)(cu_count() * Occ<PL>::W);
+    hipLaunchKernelGGL((seg_stats_list_full_kernel<PL>), dim3(blocks), dim3(256), 0, st, segs, list, cls, out);
+}
+
 template <int NMAX>
 __global__ __launch_bounds__(256) void seg_stats_exact_list_kernel(RaggedSegs segs,
                                                                    const uint32_t* list,
@@ -442,6 +516,8 @@ hipError_t launch_exact_list(const RaggedSegs& segs, const uint32_t* list, const
 void ragged_launch_lane(int n, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
                         bool aligned16, const nvrx_stats_soa& out, hipStream_t st);
 void ragged_launch_list(int pl, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
+                        const nvrx_stats_soa& out, hipStream_t st);
+void ragged_launch_full(int pl, const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
                         const nvrx_stats_soa& out, hipStream_t st);
 hipError_t ragged_launch_exact(const RaggedSegs& segs, const uint32_t* list, const uint32_t* cls,
                                int64_t max_len, const nvrx_stats_soa& out,
