@@ -156,12 +156,13 @@ struct Capture {
     int64_t ring_pci = -2;  // the ring's device (QueueInfo::pci): only its queues take ring records
     std::vector<int64_t> ring_val;
     std::vector<uint8_t> ring_busy;
+    std::vector<uint64_t> ring_last_end;  // end_ts of each record's last harvested hand-out
     uint64_t ring_next = 0;
     amd_signal_t* ring_host = nullptr;  // pinned mirror the harvest copies into
     hipStream_t ring_stream = nullptr;
     bool ring_tried = false;
     std::mutex ring_copy_mu;            // one harvest copy at a time
-    std::atomic<uint64_t> n_ring{0}, n_ring_full{0}, n_ring_bad{0};
+    std::atomic<uint64_t> n_ring{0}, n_ring_full{0}, n_ring_bad{0}, n_ring_torn{0};
     rocprofiler_client_id_t* client = nullptr;
 };
 
@@ -621,6 +622,7 @@ void ring_setup() {  // on a caller's thread (HIP calls allowed), before the fir
     std::lock_guard<std::mutex> lk(c.pmu);
     c.ring_val.assign((size_t)n, RING_INIT);
     c.ring_busy.assign((size_t)n, 0);
+    c.ring_last_end.assign((size_t)n, 0);
     c.ring_host = static_cast<amd_signal_t*>(m);
     c.ring_stream = st;
     c.ring_n = n;
@@ -658,44 +660,57 @@ void q_harvest(nvrx_profiler* p) {
     batch.clear();
     ring_ns.clear();
     std::unique_lock<std::mutex> copy_lk(c.ring_copy_mu);  // the mirror is shared
-    // the hand-out range of the ring records pending now
-    bool any_ring = false;
-    uint64_t lo = ~0ull, hi = 0;
-    {
-        std::lock_guard<std::mutex> lk(c.pmu);
-        for (const auto& e : c.pending)
-            if (e.slot >= 0) {
-                any_ring = true;
-                lo = std::min(lo, e.seq);
-                hi = std::max(hi, e.seq + 1);
-            }
-    }
-    const bool copied = any_ring && ring_copy(lo, hi);
-    {
-        std::lock_guard<std::mutex> lk(c.pmu);
-        size_t w = 0;
-        for (size_t i = 0; i < c.pending.size(); ++i) {
-            const Capture::Pending& e = c.pending[i];
-            bool complete = false;
-            if (e.slot < 0) {
-                complete = qf.load(e.sig) == 0;
-            } else if (copied && e.seq >= lo && e.seq < hi) {
-                const amd_signal_t& r = c.ring_host[e.slot];
-                complete = r.value <= e.want;
-                if (complete) {
-                    if (r.value != e.want) c.n_ring_bad.fetch_add(1, std::memory_order_relaxed);
-                    const double npt = static_cast<const QueueInfo*>(e.queue)->ns_per_tick;
-                    ring_ns.push_back(r.end_ts > r.start_ts && npt > 0.0
-                                          ? (uint64_t)((double)(r.end_ts - r.start_ts) * npt + 0.5) : 0);
-                    c.ring_busy[e.slot] = 0;
+    // A record copied while the packet processor was writing it could show the new value with a
+    // timestamp of its previous hand-out (the copy engine reads the line in its own order): a
+    // record counts as completed only with start_ts after that hand-out's end and end_ts >= start_ts;
+    // one that shows the value but not yet the timestamps is read again (at most twice more).
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        // the hand-out range of the ring records pending now
+        bool any_ring = false;
+        uint64_t lo = ~0ull, hi = 0;
+        {
+            std::lock_guard<std::mutex> lk(c.pmu);
+            for (const auto& e : c.pending)
+                if (e.slot >= 0) {
+                    any_ring = true;
+                    lo = std::min(lo, e.seq);
+                    hi = std::max(hi, e.seq + 1);
                 }
-            }
-            if (complete)
-                done.push_back(e);
-            else
-                c.pending[w++] = e;
         }
-        c.pending.resize(w);
+        const bool copied = any_ring && ring_copy(lo, hi);
+        uint64_t torn = 0;
+        {
+            std::lock_guard<std::mutex> lk(c.pmu);
+            size_t w = 0;
+            for (size_t i = 0; i < c.pending.size(); ++i) {
+                const Capture::Pending& e = c.pending[i];
+                bool complete = false;
+                if (e.slot < 0) {
+                    complete = attempt == 0 && qf.load(e.sig) == 0;
+                } else if (copied && e.seq >= lo && e.seq < hi) {
+                    const amd_signal_t& r = c.ring_host[e.slot];
+                    if (r.value <= e.want) {
+                        if (r.start_ts > c.ring_last_end[e.slot] && r.end_ts >= r.start_ts) {
+                            complete = true;
+                            if (r.value != e.want) c.n_ring_bad.fetch_add(1, std::memory_order_relaxed);
+                            const double npt = static_cast<const QueueInfo*>(e.queue)->ns_per_tick;
+                            ring_ns.push_back(npt > 0.0 ? (uint64_t)((double)(r.end_ts - r.start_ts) * npt + 0.5) : 0);
+                            c.ring_last_end[e.slot] = r.end_ts;
+                            c.ring_busy[e.slot] = 0;
+                        } else {
+                            ++torn;
+                        }
+                    }
+                }
+                if (complete)
+                    done.push_back(e);
+                else
+                    c.pending[w++] = e;
+            }
+            c.pending.resize(w);
+        }
+        if (torn == 0) break;
+        c.n_ring_torn.fetch_add(torn, std::memory_order_relaxed);
     }
     copy_lk.unlock();
     if (done.empty()) return;
