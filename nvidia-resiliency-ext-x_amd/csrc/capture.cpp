@@ -142,12 +142,13 @@ struct Capture {
     std::atomic<bool> qactive{false};     // the profiler is started
     std::atomic<bool> q_installed{false}; // hsa_queue_create is ours
     std::atomic<uint64_t> n_queues{0}, n_signals{0}, n_signal_fail{0}, n_chained{0};
-    double tick_ns = 0.0;                 // ns per HSA system timestamp tick (first harvest)
+    double tick_ns = 0.0;                 // ns per HSA system timestamp tick (first harvest; ring_copy_mu)
     // NVRX_CAPTURE_QUEUE_DIAG (cost attribution only; outputs wrong): 1 = intercept, no signals;
     // 2 = signals on queues without profiling (no timestamps)
     int qdiag = 0;
     // raw timestamps: the CP's start_ts / end_ts read from the signal itself (amd_signal_t) in GPU
-    // ticks, checked against hsa_amd_profiling_get_dispatch_time on the first harvest (-1: not yet)
+    // ticks, checked against hsa_amd_profiling_get_dispatch_time on the first harvest (-1: not yet;
+    // ring_copy_mu)
     int raw_ok = -1;
     // the ring of completion records in device memory (queue delivery, "Completion records" below):
     // ring_val = the value each record holds once its last hand-out has completed (host, pmu)
@@ -659,7 +660,7 @@ void q_harvest(nvrx_profiler* p) {
     done.clear();
     batch.clear();
     ring_ns.clear();
-    std::unique_lock<std::mutex> copy_lk(c.ring_copy_mu);  // the mirror is shared
+    std::lock_guard<std::mutex> copy_lk(c.ring_copy_mu);  // the mirror is shared
     // A record copied while the packet processor was writing it could show the new value with a
     // timestamp of its previous hand-out (the copy engine reads the line in its own order): a
     // record counts as completed only with start_ts after that hand-out's end and end_ts >= start_ts;
@@ -712,7 +713,7 @@ void q_harvest(nvrx_profiler* p) {
         if (torn == 0) break;
         c.n_ring_torn.fetch_add(torn, std::memory_order_relaxed);
     }
-    copy_lk.unlock();
+    // (copy_lk is held to the end: it also guards tick_ns and raw_ok)
     if (done.empty()) return;
     if (c.tick_ns == 0.0) {
         uint64_t f = 0;
