@@ -264,6 +264,10 @@ struct nvrx_profiler {
     int64_t log_n = 0, log_cap = 0;
     nvrx_record* h_pinned = nullptr;  // pinned staging of the host -> device drain
     int64_t pinned_cap = 0;
+    // pinned staging of a report's small transfers: the bucketing's stream offsets up, the six
+    // statistics columns down in one copy (pageable copies each cost a blocking round trip)
+    char* h_small = nullptr;
+    size_t small_bytes = 0;
     // work buffers (grown on demand)
     void* d_work = nullptr;
     size_t work_bytes = 0;
@@ -329,6 +333,19 @@ int ensure_work(nvrx_profiler* p, size_t bytes) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// p->h_small holding at least `bytes` (grown on demand)
+int ensure_small(nvrx_profiler* p, size_t bytes) {
+    if (bytes <= p->small_bytes) return NVRX_OK;
+    if (p->h_small) (void)hipHostFree(p->h_small);
+    p->h_small = nullptr;
+    p->small_bytes = 0;
+    const size_t b = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipHostMalloc((void**)&p->h_small, b, 0);
+    if (e != hipSuccess) return hip_status(e, "nvrx_profiler: hipHostMalloc(small staging)");
+    p->small_bytes = b;
+    return NVRX_OK;
+}
+
 struct Work {  // carve of d_work for one bucket + stats pass over the record log
     int64_t* rec_off;
     int64_t* seg_off;
@@ -372,8 +389,13 @@ int bucket_log(nvrx_profiler* p, int64_t nslots, int force_stable, Work& w) {
     int rc = ensure_work(p, probe.bytes);
     if (rc) return rc;
     w = carve((char*)p->d_work, nslots, ns_cap);
-    int64_t off[2] = {0, p->log_n};
-    hipError_t e = hipMemcpyAsync(w.rec_off, off, sizeof(off), hipMemcpyHostToDevice, p->stream);
+    // sized here for get_stats' download too (h_small is never reallocated under a pending copy)
+    rc = ensure_small(p, std::max<size_t>(2 * sizeof(int64_t), 6 * align256((size_t)nslots * 4)));
+    if (rc) return rc;
+    int64_t* off = (int64_t*)p->h_small;  // (the previous use of h_small has completed: synchronous calls)
+    off[0] = 0;
+    off[1] = p->log_n;
+    hipError_t e = hipMemcpyAsync(w.rec_off, off, 2 * sizeof(int64_t), hipMemcpyHostToDevice, p->stream);
     if (e != hipSuccess) return hip_status(e, "nvrx_profiler: rec_off upload");
     e = nvrx::records_bucket(p->d_log, w.rec_off, 1, nslots, p->cfg.stats_max_len_per_kernel,
                              force_stable, w.seg_off, w.seg_len, w.ns, w.counts, p->stream);
@@ -580,6 +602,7 @@ int nvrx_profiler_destroy(nvrx_profiler* p) {
         if (p->d_log) (void)hipFree(p->d_log);
         if (p->d_work) (void)hipFree(p->d_work);
         if (p->h_pinned) (void)hipHostFree(p->h_pinned);
+        if (p->h_small) (void)hipHostFree(p->h_small);
         if (p->ingest_ev) (void)hipEventDestroy(p->ingest_ev);
         if (p->stream) (void)hipStreamDestroy(p->stream);
     }
@@ -745,20 +768,19 @@ int nvrx_profiler_get_stats(nvrx_profiler* p, int64_t cap_out, int64_t* count, u
                                                       std::min<int64_t>(cap, p->log_n), cap,
                                                       p->cfg.mode, true, soa, nullptr, 0, p->stream);
             if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: segment_stats");
-            const size_t nb = (size_t)nslots * 4;
-            std::vector<int32_t> hnum(nslots);
-            std::vector<float> hmn(nslots), hmx(nslots), hmed(nslots), havg(nslots), hsd(nslots);
-            struct {
-                void* dst;
-                const void* src;
-            } cps[] = {{hnum.data(), w.num}, {hmn.data(), w.mn},   {hmx.data(), w.mx},
-                       {hmed.data(), w.med}, {havg.data(), w.avg}, {hsd.data(), w.sd}};
-            for (auto& c : cps) {
-                e = hipMemcpyAsync(c.dst, c.src, nb, hipMemcpyDeviceToHost, p->stream);
-                if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: download");
-            }
-            e = hipStreamSynchronize(p->stream);
-            if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: sync");
+            // the six columns are consecutive in the carve (num, mn, mx, med, avg, sd, each
+            // 256-B aligned): one copy into pinned staging, one synchronisation
+            const size_t span = (size_t)((char*)(w.sd + nslots) - (char*)w.num);
+            rc = ensure_small(p, span);
+            if (rc) return rc;
+            e = hipMemcpyAsync(p->h_small, w.num, span, hipMemcpyDeviceToHost, p->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+            if (e != hipSuccess) return hip_status(e, "nvrx_profiler_get_stats: download");
+            const auto col = [&](const void* d) { return p->h_small + ((const char*)d - (const char*)w.num); };
+            const int32_t* hnum = (const int32_t*)col(w.num);
+            const float *hmn = (const float*)col(w.mn), *hmx = (const float*)col(w.mx),
+                        *hmed = (const float*)col(w.med), *havg = (const float*)col(w.avg),
+                        *hsd = (const float*)col(w.sd);
             // std::map order of getStats (CuptiProfiler.cpp:137-145): sorted by composite name
             for (int64_t s = 0; s < nslots; ++s)
                 if (hnum[s] > 0) p->c_slot.push_back((uint32_t)s);

@@ -199,8 +199,13 @@ class ReportGenerator:
         f64_in = np.concatenate([kmed, kavg, smed])
         i32_in = np.concatenate([np.minimum(knum, np.iinfo(np.int32).max).astype(np.int32),
                                  kid, sid, kslot, sslot]).astype(np.int32)
-        f64_d = torch.from_numpy(f64_in).to(dev, non_blocking=False)
-        i32_d = torch.from_numpy(i32_in).to(dev, non_blocking=False)
+        # (pinned staging: asynchronous copies, ordered before the kernels on the stream)
+        pin = dev.type == "cuda"
+        f64_h, i32_h = torch.from_numpy(f64_in), torch.from_numpy(i32_in)
+        if pin:
+            f64_h, i32_h = f64_h.pin_memory(), i32_h.pin_memory()
+        f64_d = f64_h.to(dev, non_blocking=pin)
+        i32_d = i32_h.to(dev, non_blocking=pin)
         d_kmed, d_kavg, d_smed = f64_d[:K], f64_d[K:2 * K], f64_d[2 * K:]
         o = 0
         d_knum = i32_d[o:o + K]; o += K  # noqa: E702

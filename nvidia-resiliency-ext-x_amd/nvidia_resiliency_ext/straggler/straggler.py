@@ -123,11 +123,22 @@ class Detector:
         off = np.zeros(len(chunks) + 1, np.int64)
         off[1:] = np.cumsum([len(c) for c in chunks])
         dev = cls.reporter._dev()
-        vals = torch.from_numpy(np.concatenate(chunks)).to(dev)
-        num, out = ops.section_stats(vals, torch.from_numpy(off).to(dev),
-                                     max(len(c) for c in chunks))
-        num = num.cpu().numpy()
-        out = out.cpu().numpy()
+        # pinned staging both ways and one synchronisation (four blocking round trips before:
+        # ~0.2-0.4 ms of a live report, tools/probe_report_breakdown.py)
+        pin = dev.type == "cuda"
+        vals_h = torch.from_numpy(np.concatenate(chunks))
+        off_h = torch.from_numpy(off)
+        if pin:
+            vals_h, off_h = vals_h.pin_memory(), off_h.pin_memory()
+        num_d, out_d = ops.section_stats(vals_h.to(dev, non_blocking=pin), off_h.to(dev, non_blocking=pin),
+                                         max(len(c) for c in chunks))
+        num_t = torch.empty(num_d.shape, dtype=num_d.dtype, pin_memory=pin)
+        out_t = torch.empty(out_d.shape, dtype=out_d.dtype, pin_memory=pin)
+        num_t.copy_(num_d, non_blocking=pin)
+        out_t.copy_(out_d, non_blocking=pin)
+        if pin:
+            torch.cuda.current_stream(dev).synchronize()
+        num, out = num_t.numpy(), out_t.numpy()
         return {n: {Statistic.MIN: float(out[0, i]), Statistic.MAX: float(out[1, i]),
                     Statistic.MED: float(out[2, i]), Statistic.AVG: float(out[3, i]),
                     Statistic.STD: float(out[4, i]), Statistic.NUM: int(num[i])}
