@@ -305,14 +305,15 @@ int nvrx_profiler_kernel_name(nvrx_profiler* p, uint32_t slot, char* buf, int64_
  * it lets a caller (the live-capture parity check) recompute the statistics elsewhere. */
 int nvrx_profiler_get_records(nvrx_profiler* p, int64_t cap_out, int64_t* count,
                               nvrx_record* out);
-/* Live kernel-dispatch capture through rocprofiler-sdk (CuptiProfiler.cpp:96-203).
- * nvrx_capture_configure registers the library as a rocprofiler-sdk tool; it must run
- * before the process's first HIP call (NVRX_ERR_STATE otherwise).  Once the runtime has
- * initialised, nvrx_profiler_capture_available() returns 1 and every kernel that completes
- * while a profiler handle is started is pushed into it under the reference's composite key
- * "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled name, block dims, grid dims in blocks, a partial
- * last block counted) with its integer-ns duration; nvrx_profiler_stop / _get_stats flush the
- * capture buffer first.  As CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL does (CuptiProfiler.cpp:118,
+/* Live kernel-dispatch capture (CuptiProfiler.cpp:96-203).  nvrx_capture_configure registers
+ * the library as a rocprofiler-sdk tool; it must run before the process's first HIP call
+ * (NVRX_ERR_STATE otherwise).  Once the runtime has initialised, nvrx_profiler_capture_available()
+ * returns 1 and every kernel enqueued while a profiler handle is started is pushed into it, once it
+ * has completed, under the reference's composite key "%s_blk_%d_%d_%d_grid_%d_%d_%d" (mangled name,
+ * block dims, grid dims in blocks, a partial last block counted) with its integer-ns duration;
+ * nvrx_profiler_stop / _get_stats flush the capture first.  By default the runtime's HSA queues are
+ * intercepted and each dispatch gets a completion record in device memory (NVRX_CAPTURE_DELIVERY=
+ * queue); callback / buffer / callback_counted use rocprofiler-sdk's kernel-dispatch tracing.  As CUPTI_ACTIVITY_KIND_CONCURRENT_KERNEL does (CuptiProfiler.cpp:118,
  * 179), copies and fills are not kernels: the ROCm runtime's blit kernels ("__amd_rocclr_*",
  * which carry out hipMemcpy* / hipMemset*) are left out unless NVRX_CAPTURE_RUNTIME_KERNELS=1. */
 int nvrx_capture_configure(void);
@@ -320,10 +321,10 @@ int nvrx_profiler_capture_available(void);
 /* Deliver the dispatch records completed so far to the started / stopped profiler
  * (cuptiActivityFlushAll(0), CuptiProfiler.cpp:138).  Synchronous; no-op without capture. */
 int nvrx_capture_flush(void);
-/* Cost accounting of the live capture since configuration (process-wide, monotone): buffer
- * callbacks delivered by rocprofiler-sdk, record headers in them, dispatch records handed to a
- * profiler, wall time spent inside this library's buffer callback, and the number and wall time
- * of rocprofiler_flush_buffer calls (report-time flushes).  No reference counterpart (CUPTI's
+/* Cost accounting of the live capture since configuration (process-wide, monotone): delivery
+ * callbacks (queue delivery: harvests), records in them, dispatch records handed to a profiler,
+ * wall time spent inside this library's delivery callbacks, and the number and wall time of
+ * report-time flushes.  No reference counterpart (CUPTI's
  * cost is not exposed either); tools/capture_cost.cpp reads it.  runtime_kernels counts the runtime
  * blit dispatches left out (above), own_kernels the library's own report kernels left out: while
  * get_stats / get_records / reset / ingest run, the dispatches of the calling thread are marked

@@ -520,7 +520,7 @@ uint32_t slot_of_name(nvrx_profiler* p, const std::string& key) {
 }  // namespace
 
 namespace nvrx {
-// capture.cpp's buffer callback: one delivered batch of completed dispatches.  A dispatch
+// the capture's delivery (capture_drain / q_harvest): one batch of completed dispatches.  A dispatch
 // enqueued while the profiler was started may complete (and its record arrive) after stop;
 // it is still counted, as CUPTI delivers the activity records of kernels launched while the
 // activity kind was enabled (bufferCompleted, CuptiProfiler.cpp:168-203, pushes regardless

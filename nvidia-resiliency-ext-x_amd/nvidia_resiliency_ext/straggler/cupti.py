@@ -4,10 +4,10 @@
 (cupti_module_py.cpp:33-54) with the nvrx_profiler handle of libnvrx_hip.so: records are
 kept as a device-resident log in HBM and reduced to per-kernel statistics by the HIP
 kernels at get_stats time (only the last ``statsMaxLenPerKernel`` records of every kernel
-count, as the reference's rings keep them).  Records enter through the rocprofiler-sdk
-kernel-dispatch capture (capture.cpp: every kernel that completes while the profiler is
-started, keyed like CuptiProfiler.cpp:182-185) and through ``push`` (external tracers,
-tests).  rocprofiler-sdk tools configure when the ROCm runtime initialises, so capture
+count, as the reference's rings keep them).  Records enter through the live capture
+(capture_queue.cpp / capture.cpp: every kernel enqueued while the profiler is started, once it
+completed, keyed like CuptiProfiler.cpp:182-185) and through ``push`` / ``ingest`` (external
+tracers, tests).  rocprofiler-sdk tools configure when the ROCm runtime initialises, so capture
 needs ``enable_capture()`` (or the first ``KernelProfiler``) before the process's first
 HIP call -- the same constraint CUPTI activity tracing has on its first CUDA context.
 
