@@ -183,11 +183,13 @@ def test_cupti_manager_refcount():
 # records_bucket (records.hip) + the length-classed ragged kernels.  (52, 8192, 900, 1100): ~52k
 # records per stream, past the 16,384 pairs a workgroup holds in VGPRs and its LDS stash, so
 # pass 2 re-reads from memory; (500, 100, ...): overflowed rings; (6000, 100, ...) / (9000, 8192,
-# ...): large slot tables, whose buckets do not all fit the LDS stage
+# ...): large slot tables, whose buckets do not all fit the LDS stage; (20, 1024, ...), (6, 2048,
+# ...), (3, 4096, ...): rings at and past a capacity of 64 * PL samples (the FULL classes)
 @pytest.mark.parametrize("nslots,cap,lo,hi", [(37, 8192, 0, 40), (37, 5, 0, 30), (3000, 0, 0, 3),
                                               (500, 100, 0, 150), (64, 8192, 60, 70),
                                               (52, 8192, 900, 1100), (6000, 100, 0, 6),
-                                              (9000, 8192, 0, 3)])
+                                              (9000, 8192, 0, 3), (20, 1024, 900, 1300),
+                                              (6, 2048, 1900, 2300), (3, 4096, 4000, 4300)])
 def test_records_stats_fused_matches_oracle(nslots, cap, lo, hi):
     # every field vs the oracle's ring-push + computeStats restatement
     rng = np.random.default_rng(nslots + cap + hi)

@@ -377,3 +377,63 @@ def test_grouped_full_segments(n, mult):
     want = O.kernel_ref(ref["num"].reshape(-1, K), ref["med"].reshape(-1, K))
     got = col.cpu().numpy()
     assert np.array_equal(got[:K].view(np.float32), want) and not got[K:].any()
+
+
+@pytest.mark.parametrize("keep,nfull", [(1024, 4 * 8300 + 3), (2048, 4 * 40 + 1), (4096, 4 * 25 + 2),
+                                        (8192, 4 * 30 + 3)])
+def test_full_class_segments(keep, nfull):
+    """The FULL classes (FAST, 16-B aligned retained runs of exactly keep = 64 * PL samples,
+    PL 16..128: seg_stats_list_full_kernel, four list entries per wave, one lane-parallel
+    epilogue): rings at capacity (length == keep) and overflowed ones (length > keep, the last
+    keep retained) mixed with the neighbouring list / lane classes; the edge distributions
+    (wide keys take the decoded moments) at the first, last and a middle entry of a group and in
+    a partial last group; for keep 1024 more entries than one sweep of the grid covers."""
+    rng = np.random.default_rng(keep + nfull)
+    nother = 300
+    lens = np.concatenate([np.where(rng.random(nfull) < 0.5, keep, keep + rng.integers(1, keep, nfull)),
+                           rng.choice([keep - 1, keep - 4, keep // 2 + 3, 100, 9], nother)]).astype(np.int64)
+    perm = rng.permutation(lens.size)
+    lens = lens[perm]
+    off = np.zeros(lens.size, np.int64)
+    pos = 0
+    for s, L in enumerate(lens):
+        keep_s = min(int(L), keep)
+        pos += (-(pos + int(L) - keep_s)) % 4  # the retained run starts 16-B aligned
+        off[s] = pos
+        pos += int(L)
+    host = rng.integers(2000, 2_200_000, size=pos + 8, dtype=np.uint32)
+    full = np.flatnonzero(lens >= keep)
+    assert full.size == nfull
+    edges = _edge_segments(keep)
+    # list positions of the FULL class follow segment order: entries 0, 3, 4, 5, the middle and
+    # the last three (the partial last group)
+    at = [0, 3, 4, 5, nfull // 2, nfull - 1, nfull - 2, nfull - 3, 9, 14]
+    for a, seg in zip(at, edges):
+        s = full[a]
+        host[off[s] + lens[s] - keep: off[s] + lens[s]] = seg
+    ns = torch.from_numpy(host.view(np.int32)).to(DEV)
+    st = ops.segment_stats_ragged(ns, torch.from_numpy(off).to(DEV),
+                                  torch.from_numpy(lens.astype(np.int32)).to(DEV),
+                                  max_len=int(lens.max()), cap=keep, mode=ops.STATS_FAST, aligned16=True)
+    g = st.cpu()
+    # the retained windows of the FULL segments as a matrix: the oracle's threaded matrix path
+    idx = (off[full] + lens[full] - keep)[:, None] + np.arange(keep)[None, :]
+    win = np.ascontiguousarray(host[idx]).reshape(-1)
+    ref = _oracle_segments(win, nfull, keep, 0, keep, 0)
+    for f in FIELDS:
+        a = getattr(g, f).numpy()[full]
+        b = ref[f]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (f, keep)
+    x = host[idx].astype(np.float64)
+    avg, std = x.mean(axis=1) / 1000.0, x.std(axis=1) / 1000.0
+    for a, _ in zip(at, edges):
+        v = key_values(host[idx[a]])
+        avg[a], std[a] = v.mean() / 1000.0, v.std() / 1000.0
+    np.testing.assert_allclose(g.avg.numpy()[full], avg, rtol=2.5e-7, atol=1e-30)
+    np.testing.assert_allclose(g.std.numpy()[full], std, rtol=1e-6, atol=1e-6 * avg.max())
+    for s in np.flatnonzero(lens < keep):  # the other classes, against computeStats
+        L = int(lens[s])
+        r = O.compute_stats(O.key_to_us(host[off[s]:off[s] + L]))
+        assert g.num[s].item() == r.num_calls == L
+        got = [np.float32(getattr(g, f)[s].item()) for f in ("min", "max", "med")]
+        assert got == [np.float32(x) for x in (r.min, r.max, r.median)], (s, L)
