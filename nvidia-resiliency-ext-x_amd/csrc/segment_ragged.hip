@@ -121,7 +121,7 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
     const uint32_t* list = cls_list;
     const int64_t need = aligned16 ? keep : keep + 3;
     // class kernels; classes that max_len rules out are not launched.  With side streams the
-    // classes are dealt round robin over them (fork / join by events, which HIP graph capture
+    // classes are dealt round robin over them in launch order (fork / join by events, which HIP graph capture
     // follows), so one class's tail and latency-bound waves overlap the next class.
     std::lock_guard<std::mutex> lock(fork_mutex());
     Fork* fk = nullptr;
@@ -132,23 +132,65 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
         return i ? fk->s[i] : st;
     };
     const uint32_t* c = cls;
-    ragged_launch_lane(8, segs, list, c + 2 * C_T8, aligned16, out, S());
-    if (keep > 8) ragged_launch_lane(16, segs, list, c + 2 * C_T16, aligned16, out, S());
-    if (keep > 16) ragged_launch_lane(32, segs, list, c + 2 * C_T32, aligned16, out, S());
-    if (keep > 32) ragged_launch_lane(64, segs, list, c + 2 * C_T64, aligned16, out, S());
-    if (keep > 64) ragged_launch_lane(128, segs, list, c + 2 * C_T128, aligned16, out, S());
+    // the launches: (kind, size); kind 0 lane<size>, 1 list<size>, 2 FULL<size / 64>, 3 workgroup
+    struct L {
+        int kind, n;
+    };
+    L lane[5], wave[6], big[2];
+    int nl = 0, nw = 0, nb = 0;
+    for (int n = 8; n <= 128; n *= 2)
+        if (n == 8 || keep > n / 2) lane[nl++] = {0, n};
     if (!exact) {
-        if (keep > 128) ragged_launch_list(4, segs, list, c + 2 * C_W4, out, S());
-        if (need > 64 * 4) ragged_launch_list(8, segs, list, c + 2 * C_W8, out, S());
-        if (need > 64 * 8) ragged_launch_list(16, segs, list, c + 2 * C_W16, out, S());
-        if (need > 64 * 16) ragged_launch_list(32, segs, list, c + 2 * C_W32, out, S());
-        if (need > 64 * 32) ragged_launch_list(64, segs, list, c + 2 * C_W64, out, S());
-        if (need > 64 * 64) ragged_launch_list(128, segs, list, c + 2 * C_W128, out, S());
-        if (const int fn = full_len(keep, aligned16, exact))  // the FULL class (seg_class)
-            ragged_launch_full(fn / 64, segs, list, c + 2 * C_F, out, S());
+        if (keep > 128) wave[nw++] = {1, 4};
+        for (int pl = 8; pl <= 128; pl *= 2)
+            if (need > 64 * (pl / 2)) wave[nw++] = {1, pl};
+        if (const int fn = full_len(keep, aligned16, exact)) big[nb++] = {2, fn};  // the FULL class
+    }
+    if (exact ? keep > 128 : need > 64 * 128) big[nb++] = {3, 0};
+    // order: the long-segment classes first, then the wave classes, then the lane classes (a FULL
+    // kernel last ran alone behind the others; DESIGN 3.2, profiles/r05/class_order_ab.log)
+#ifndef NVRX_CLASS_ORDER  // build-time tuning constant (timing A/B of the launch order)
+#define NVRX_CLASS_ORDER 2
+#endif
+    L order[13];
+    int no = 0;
+    const auto put = [&](const L* a, int n, bool rev) {
+        for (int i = 0; i < n; ++i) order[no++] = a[rev ? n - 1 - i : i];
+    };
+    switch (NVRX_CLASS_ORDER) {
+        case 0: put(lane, nl, false); put(wave, nw, false); put(big, nb, false); break;
+        case 1: put(big, nb, false); put(lane, nl, false); put(wave, nw, false); break;
+        case 2: put(big, nb, false); put(wave, nw, false); put(lane, nl, false); break;
+        case 3: put(big, nb, false); put(wave, nw, true); put(lane, nl, true); break;
+        case 4: put(big, nb, false); put(lane, nl, true); put(wave, nw, true); break;
+        case 6: put(big, nb, false); put(wave, nw, false); put(lane, nl, true); break;
+        default: {  // 5: big first, then wave and lane classes interleaved, longest first
+            put(big, nb, false);
+            for (int i = 0; i < std::max(nl, nw); ++i) {
+                if (i < nw) order[no++] = wave[nw - 1 - i];
+                if (i < nl) order[no++] = lane[nl - 1 - i];
+            }
+        }
     }
     hipError_t e = hipSuccess;
-    if (exact ? keep > 128 : need > 64 * 128) e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, S());
+    for (int i = 0; i < no && e == hipSuccess; ++i) {
+        const L& o = order[i];
+        switch (o.kind) {
+            case 0: {
+                const int cl = o.n == 8 ? C_T8 : o.n == 16 ? C_T16 : o.n == 32 ? C_T32 : o.n == 64 ? C_T64 : C_T128;
+                ragged_launch_lane(o.n, segs, list, c + 2 * cl, aligned16, out, S());
+                break;
+            }
+            case 1: {
+                const int cl = o.n == 4 ? C_W4 : o.n == 8 ? C_W8 : o.n == 16 ? C_W16 : o.n == 32 ? C_W32
+                             : o.n == 64 ? C_W64 : C_W128;
+                ragged_launch_list(o.n, segs, list, c + 2 * cl, out, S());
+                break;
+            }
+            case 2: ragged_launch_full(o.n / 64, segs, list, c + 2 * C_F, out, S()); break;
+            default: e = ragged_launch_exact(segs, list, c + 2 * C_X, keep, out, S());
+        }
+    }
     if (e == hipSuccess) e = hipGetLastError();
     // joined on every path: a side stream left forked would leave a graph capture unjoined
     if (fk) {
