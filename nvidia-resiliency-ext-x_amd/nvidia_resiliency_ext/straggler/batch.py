@@ -382,62 +382,17 @@ def _warm_up(rep: MatrixReporter, stats) -> None:
 # NVRX_PIPE_D2H=copy: pipelined reports write a device buffer and copy it to the pinned one
 # (one more graph node) instead of the scores kernel writing pinned host memory directly
 _PIPE_COPY = os.environ.get("NVRX_PIPE_D2H", "") == "copy"
-# NVRX_PIPE_OVERLAP=0: pipelined reports as whole-report graphs on one stream (round 4) instead
-# of the statistics and the scores phases on two streams (timing A/B)
-_PIPE_OVERLAP = os.environ.get("NVRX_PIPE_OVERLAP", "1") != "0"
 
 TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
-
-
-class _Slot:
-    """The buffers one report in flight shares between its statistics and its scores phase:
-    segment statistics, column reference (+ its f32 form), the scores epilogue's completion
-    counter.  Slot 0 is the reporter's own set; `clean` mirrors MatrixReporter._colref_clean for
-    this slot's column reference."""
-
-    def __init__(self, rep: MatrixReporter, primary: bool):
-        self.primary = primary
-        if primary:
-            self.stats, self.col_ref, self.ref_f32, self.done = rep.stats, rep.col_ref, rep._ref_f32, rep.done
-            self.clean = rep._colref_clean
-        else:
-            self.stats = ops.SegmentStats.empty(rep.R * rep.K, rep.device)
-            self.col_ref = torch.empty_like(rep.col_ref)
-            self.ref_f32 = torch.empty_like(rep._ref_f32)
-            self.done = torch.zeros_like(rep.done)
-            self.clean = False  # uninitialised: its first statistics phase initialises it
-
-    def bind(self, rep: MatrixReporter):
-        """Context: rep's statistics / reference buffers are this slot's (graph capture bakes
-        them into the captured kernels)."""
-        slot = self
-
-        class _Bound:
-            def __enter__(self):
-                self.saved = (rep.stats, rep.col_ref, rep._ref_f32, rep.done, rep._colref_clean)
-                rep.stats, rep.col_ref, rep._ref_f32, rep.done = slot.stats, slot.col_ref, slot.ref_f32, slot.done
-                rep._colref_clean = slot.clean
-
-            def __exit__(self, *exc):
-                slot.clean = rep._colref_clean
-                rep.stats, rep.col_ref, rep._ref_f32, rep.done = self.saved[:4]
-                rep._colref_clean = slot.clean if slot.primary else self.saved[4]
-                return False
-
-        return _Bound()
 
 
 class PipelinedReports:
     """Full reports as HIP graphs, two in flight (1 GPU).  Each report -- column-reference init,
     statistics, scores + straggler masks -- ends with the device-to-host copy of the packed
     results into one of two pinned buffers, so the host can read report i while report i+1
-    runs: the GPU sees back-to-back reports instead of one report per host round trip.
-    Overlap (default): report i's two phases run as two graphs on two streams -- the
-    statistics on the caller's stream, back to back with report i+1's, the scores (and the
-    individual history, hence in submission order) on a side stream once report i's statistics
-    are done -- with the statistics / reference buffers doubled (one set per report in flight),
-    so report i's scores run beside report i+1's statistics instead of between them.
-    NVRX_PIPE_OVERLAP=0: one whole-report graph per report on one stream (round 4).
+    runs: the GPU sees back-to-back reports instead of one report per host round trip.  Report
+    order on the device is the submission order (one stream), so the individual history
+    advances exactly as with report().
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
@@ -452,18 +407,9 @@ class PipelinedReports:
         self.rep, self.timing = rep, timing
         if stats is None:
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
-        self.overlap = _PIPE_OVERLAP
+        _warm_up(rep, stats)
+        self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
-
-        def scores(k: int):
-            # the scores kernel writes the pinned buffer itself when its epilogue stores the
-            # error word (fused reference, R <= FUSED_REF_MAX_ROWS); otherwise the error word is
-            # zeroed on the device first and the results copied
-            if _PIPE_COPY or not rep._fuse_ref():
-                rep.compute_scores()
-                self.bufs[k].copy_(rep.out, non_blocking=True)
-            else:
-                rep.compute_scores(out_buf=self.bufs[k])
 
         def capture(with_stats: bool, rest: bool, k: int):
             g = torch.cuda.CUDAGraph()
@@ -471,30 +417,21 @@ class PipelinedReports:
                 if with_stats:
                     stats()
                 if rest:
-                    scores(k)
+                    # the scores kernel writes the pinned buffer itself when its epilogue stores
+                    # the error word (fused reference, R <= FUSED_REF_MAX_ROWS); otherwise the
+                    # error word is zeroed on the device first and the results copied
+                    if _PIPE_COPY or not rep._fuse_ref():
+                        rep.compute_scores()
+                        self.bufs[k].copy_(rep.out, non_blocking=True)
+                    else:  # the scores kernel writes the pinned buffer itself
+                        rep.compute_scores(out_buf=self.bufs[k])
             return g
 
-        if self.overlap:
-            self.slots = [_Slot(rep, True), _Slot(rep, False)]
-            self.stats_g, self.rest_g = [], []
-            for k, slot in enumerate(self.slots):
-                with slot.bind(rep):
-                    _warm_up(rep, stats)  # initialises this slot's column reference too
-                    self.stats_g.append(capture(True, False, k))
-                    self.rest_g.append(capture(False, True, k))
-            self._needs_clean = rep._colref_clean
-            self.side = torch.cuda.Stream(rep.device)
-            self.stats_done = [torch.cuda.Event() for _ in range(2)]
-            if timing:
-                self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        else:
-            _warm_up(rep, stats)
-            self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
-            self.full = [capture(True, True, k) for k in range(2)]
-            if timing:
-                self.stats = capture(True, False, 0)
-                self.rest = [capture(False, True, k) for k in range(2)]
-                self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        self.full = [capture(True, True, k) for k in range(2)]
+        if timing:
+            self.stats = capture(True, False, 0)
+            self.rest = [capture(False, True, k) for k in range(2)]
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.done = [torch.cuda.Event() for _ in range(2)]
         self.pending = []  # (slot, timed) in flight, oldest first
         self.ready = []    # results collected early (a timed submit drains), oldest first
@@ -507,10 +444,10 @@ class PipelinedReports:
         if self._needs_clean and not self.rep._colref_clean:
             raise RuntimeError("PipelinedReports: an unpaired statistics phase (ReportGraph."
                                "run_stats without run_rest) left the column reference in use")
-        if timed and not self.timing:
-            raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
         k = self.n & 1
         if timed:
+            if not self.timing:
+                raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
             while self.pending:  # the device idles before the measured statistics phase
                 self.ready.append(self._land())
             # a short spin keeps the device busy while the host queues the graphs, so the
@@ -519,29 +456,14 @@ class PipelinedReports:
             spin = getattr(torch.cuda, "_sleep", None)  # torch's spin kernel (private API)
             if spin is not None:
                 spin(TIMED_SPIN_CYCLES)
-        if self.overlap:
-            main = torch.cuda.current_stream(self.rep.device)
-            main.wait_event(self.done[k])  # slot k's previous report has read its statistics
-            if timed:
-                self.ev[0].record(main)
-            self.stats_g[k].replay()
-            if timed:
-                self.ev[1].record(main)
-            self.stats_done[k].record(main)
-            self.side.wait_event(self.stats_done[k])
-            with torch.cuda.stream(self.side):
-                self.rest_g[k].replay()
-            self.done[k].record(self.side)
+            self.ev[0].record()
+            self.stats.replay()
+            self.ev[1].record()
+            self.rest[k].replay()
         else:
-            if timed:
-                self.ev[0].record()
-                self.stats.replay()
-                self.ev[1].record()
-                self.rest[k].replay()
-            else:
-                self.full[k].replay()
-            self.done[k].record()
+            self.full[k].replay()
         self.rep._colref_clean = self.rep._fuse_ref()
+        self.done[k].record()
         self.pending.append((k, timed))
         self.n += 1
 
@@ -553,8 +475,6 @@ class PipelinedReports:
         else:
             while not ev.query():
                 pass
-        if self.overlap:  # later work on the caller's stream sees this report's history update
-            torch.cuda.current_stream(self.rep.device).wait_event(ev)
         ms = self.ev[0].elapsed_time(self.ev[1]) if timed else None
         return self.rep._unpack(self.bufs[k]), ms
 
