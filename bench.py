@@ -220,7 +220,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed,
                     kern_ms=float(np.mean(ks)) if ks else None,
                     samples=R * K_local * keep, nseg=R * K_local, keep=keep,
-                    launch="hip_graph: whole reports, two in flight", phases=phases)
+                    launch=pipe_label(pipe), phases=phases)
     # N GPUs: the statistics, the shard's score partials and the combine replay as HIP graphs;
     # only the all_gather of the partials between them is an eager collective
     g = rep.graph(ns, s_push) if use_graph else None
@@ -249,6 +249,13 @@ def gather_labels(label: str, world: int):
     out = [None] * world
     torch.distributed.all_gather_object(out, label)
     return out
+
+
+def pipe_label(pipe) -> str:
+    """The launch label of a batch.PipelinedReports loop."""
+    if getattr(pipe, "alt", False):
+        return "hip_graph: whole reports, two in flight on two streams"
+    return "hip_graph: whole reports, two in flight"
 
 
 def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
@@ -289,7 +296,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
             pipe.submit(timed=True)
             ks.append(pipe.collect()[1])
         stats_ms = float(np.mean(ks))
-        launch = "hip_graph: whole reports, two in flight"
+        launch = pipe_label(pipe)
     else:
         # N GPUs: as the other legs -- statistics, score partials and combine as HIP graphs,
         # the all_gather of the partials eager between them

@@ -382,17 +382,73 @@ def _warm_up(rep: MatrixReporter, stats) -> None:
 # NVRX_PIPE_D2H=copy: pipelined reports write a device buffer and copy it to the pinned one
 # (one more graph node) instead of the scores kernel writing pinned host memory directly
 _PIPE_COPY = os.environ.get("NVRX_PIPE_D2H", "") == "copy"
+# NVRX_PIPE_MODE=whole: pipelined reports as whole-report graphs on one stream (round 4) instead
+# of each report on its own stream of two (timing A/B)
+_PIPE_ALT = os.environ.get("NVRX_PIPE_MODE", "alt") != "whole"
 
 TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
 
 
+class _Slot:
+    """The buffers of one report in flight: segment statistics, column reference (+ its f32
+    form), the scores epilogue's completion counter, the record-stream bucketing output.  Slot
+    0 is the reporter's own set; `clean` mirrors MatrixReporter._colref_clean for this slot's
+    column reference."""
+
+    def __init__(self, rep: MatrixReporter, primary: bool):
+        self.primary = primary
+        if primary:
+            self.stats, self.col_ref, self.ref_f32, self.done = rep.stats, rep.col_ref, rep._ref_f32, rep.done
+            self.clean = rep._colref_clean
+        else:
+            self.stats = ops.SegmentStats.empty(rep.R * rep.K, rep.device)
+            self.col_ref = torch.empty_like(rep.col_ref)
+            self.ref_f32 = torch.empty_like(rep._ref_f32)
+            self.done = torch.zeros_like(rep.done)
+            self.clean = False  # uninitialised: its first statistics phase initialises it
+        self.bucket = getattr(rep, "_bucket", None) if primary else None
+
+    _FIELDS = ("stats", "col_ref", "_ref_f32", "done", "_bucket")
+
+    def _mine(self):
+        return (self.stats, self.col_ref, self.ref_f32, self.done, self.bucket)
+
+    def bind(self, rep: MatrixReporter):
+        """Context: rep's buffers are this slot's (graph capture bakes them into the kernels)."""
+        slot = self
+
+        class _Bound:
+            def __enter__(self):
+                self.saved = tuple(getattr(rep, f, None) for f in _Slot._FIELDS) + (rep._colref_clean,)
+                for f, v in zip(_Slot._FIELDS, slot._mine()):
+                    setattr(rep, f, v)
+                rep._colref_clean = slot.clean
+
+            def __exit__(self, *exc):
+                slot.clean, slot.bucket = rep._colref_clean, getattr(rep, "_bucket", None)
+                for f, v in zip(_Slot._FIELDS, self.saved):
+                    setattr(rep, f, v)
+                if slot.primary:  # the reporter's own set: its state is the slot's
+                    rep._bucket = slot.bucket
+                    rep._colref_clean = slot.clean
+                else:
+                    rep._colref_clean = self.saved[-1]
+                return False
+
+        return _Bound()
+
+
 class PipelinedReports:
     """Full reports as HIP graphs, two in flight (1 GPU).  Each report -- column-reference init,
-    statistics, scores + straggler masks -- ends with the device-to-host copy of the packed
-    results into one of two pinned buffers, so the host can read report i while report i+1
-    runs: the GPU sees back-to-back reports instead of one report per host round trip.  Report
-    order on the device is the submission order (one stream), so the individual history
-    advances exactly as with report().
+    statistics, scores + straggler masks -- ends with its packed results landing in one of two
+    pinned host buffers, so the host can read report i while report i+1 runs: the GPU sees
+    back-to-back reports instead of one report per host round trip.
+    Two streams (default): report i runs on stream i % 2 with its own set of statistics /
+    reference buffers (_Slot), so report i+1's statistics kernel starts while report i's drains
+    instead of after it (the launch-to-launch transition of one stream); report i's scores wait
+    for report i-1's, so the individual history advances in submission order.  The inputs a
+    report reads must not change until it is collected (collect() orders the caller's stream
+    after it).  NVRX_PIPE_MODE=whole: one whole-report graph per report on the caller's stream.
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
@@ -407,9 +463,18 @@ class PipelinedReports:
         self.rep, self.timing = rep, timing
         if stats is None:
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
-        _warm_up(rep, stats)
-        self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
+        self.alt = _PIPE_ALT
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
+
+        def scores(k: int):
+            # the scores kernel writes the pinned buffer itself when its epilogue stores the
+            # error word (fused reference, R <= FUSED_REF_MAX_ROWS); otherwise the error word is
+            # zeroed on the device first and the results copied
+            if _PIPE_COPY or not rep._fuse_ref():
+                rep.compute_scores()
+                self.bufs[k].copy_(rep.out, non_blocking=True)
+            else:
+                rep.compute_scores(out_buf=self.bufs[k])
 
         def capture(with_stats: bool, rest: bool, k: int):
             g = torch.cuda.CUDAGraph()
@@ -417,20 +482,27 @@ class PipelinedReports:
                 if with_stats:
                     stats()
                 if rest:
-                    # the scores kernel writes the pinned buffer itself when its epilogue stores
-                    # the error word (fused reference, R <= FUSED_REF_MAX_ROWS); otherwise the
-                    # error word is zeroed on the device first and the results copied
-                    if _PIPE_COPY or not rep._fuse_ref():
-                        rep.compute_scores()
-                        self.bufs[k].copy_(rep.out, non_blocking=True)
-                    else:  # the scores kernel writes the pinned buffer itself
-                        rep.compute_scores(out_buf=self.bufs[k])
+                    scores(k)
             return g
 
-        self.full = [capture(True, True, k) for k in range(2)]
+        if self.alt:
+            self.slots = [_Slot(rep, True), _Slot(rep, False)]
+            self.stats_g, self.rest_g = [], []
+            for k, slot in enumerate(self.slots):
+                with slot.bind(rep):
+                    _warm_up(rep, stats)  # initialises this slot's column reference too
+                    self.stats_g.append(capture(True, False, k))
+                    self.rest_g.append(capture(False, True, k))
+            self._needs_clean = rep._colref_clean
+            self.streams = [torch.cuda.Stream(rep.device) for _ in range(2)]
+        else:
+            _warm_up(rep, stats)
+            self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
+            self.full = [capture(True, True, k) for k in range(2)]
+            if timing:
+                self.stats = capture(True, False, 0)
+                self.rest = [capture(False, True, k) for k in range(2)]
         if timing:
-            self.stats = capture(True, False, 0)
-            self.rest = [capture(False, True, k) for k in range(2)]
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.done = [torch.cuda.Event() for _ in range(2)]
         self.pending = []  # (slot, timed) in flight, oldest first
@@ -444,10 +516,10 @@ class PipelinedReports:
         if self._needs_clean and not self.rep._colref_clean:
             raise RuntimeError("PipelinedReports: an unpaired statistics phase (ReportGraph."
                                "run_stats without run_rest) left the column reference in use")
+        if timed and not self.timing:
+            raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
         k = self.n & 1
         if timed:
-            if not self.timing:
-                raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
             while self.pending:  # the device idles before the measured statistics phase
                 self.ready.append(self._land())
             # a short spin keeps the device busy while the host queues the graphs, so the
@@ -456,14 +528,30 @@ class PipelinedReports:
             spin = getattr(torch.cuda, "_sleep", None)  # torch's spin kernel (private API)
             if spin is not None:
                 spin(TIMED_SPIN_CYCLES)
-            self.ev[0].record()
-            self.stats.replay()
-            self.ev[1].record()
-            self.rest[k].replay()
+        if self.alt:
+            s = self.streams[k]
+            # the caller's work so far (inputs; the wait for the collected reports) comes first;
+            # slot k's previous report ran on this stream
+            s.wait_stream(torch.cuda.current_stream(self.rep.device))
+            with torch.cuda.stream(s):
+                if timed:
+                    self.ev[0].record(s)
+                self.stats_g[k].replay()
+                if timed:
+                    self.ev[1].record(s)
+                s.wait_event(self.done[k ^ 1])  # report i-1's scores: the history's order
+                self.rest_g[k].replay()
+            self.done[k].record(s)
         else:
-            self.full[k].replay()
+            if timed:
+                self.ev[0].record()
+                self.stats.replay()
+                self.ev[1].record()
+                self.rest[k].replay()
+            else:
+                self.full[k].replay()
+            self.done[k].record()
         self.rep._colref_clean = self.rep._fuse_ref()
-        self.done[k].record()
         self.pending.append((k, timed))
         self.n += 1
 
@@ -475,6 +563,8 @@ class PipelinedReports:
         else:
             while not ev.query():
                 pass
+        if self.alt:  # the caller's later work (new inputs, the history) follows this report
+            torch.cuda.current_stream(self.rep.device).wait_event(ev)
         ms = self.ev[0].elapsed_time(self.ev[1]) if timed else None
         return self.rep._unpack(self.bufs[k]), ms
 

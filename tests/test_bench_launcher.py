@@ -78,8 +78,9 @@ def test_launcher_four_ranks_gloo_rehearsal():
     assert gp["launch_per_rank"] == [want] * 4 and gp["straggler_sets_exact"] is True
     assert line["ms_per_step_graph_phases"] == line["ms_per_step"]
     one = _run(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
-    assert one["zipf_16384_ranks"]["launch_per_rank"] == ["hip_graph: whole reports, two in flight"]
-    assert one["config"]["launch"] == "hip_graph: whole reports, two in flight"
+    pipelined = "hip_graph: whole reports, two in flight on two streams"
+    assert one["zipf_16384_ranks"]["launch_per_rank"] == [pipelined]
+    assert one["config"]["launch"] == pipelined
     assert one["graph_phases"]["launch_per_rank"] == ["hip_graph: statistics | rest"]
     assert one["graph_phases"]["straggler_sets_exact"] is True
     assert one["ms_per_step_graph_phases"] > 0
