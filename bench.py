@@ -608,7 +608,10 @@ def main():
                          "traffic": traffic,
                          "kernel": "seg_stats_lean_group_kernel<128> (4 segments per wave)",
                          "kernel_ms": kern_ms,
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes,
+                         # the same bytes over the pipelined loop's time per report (two reports'
+                         # statistics kernels overlap at their boundaries)
+                         "per_report_frac": alg_bytes / (ms_per_step * 1e-3) / HBM_PEAK},
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,
             "configs0_report": c1,
