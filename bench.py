@@ -132,7 +132,7 @@ def warm(step, n_min: int, world: int) -> int:
 
 
 def phases_loop(rep, ns, s_push, g, steps, world, time_kernel):
-    """The N-GPU launch mode: per report the statistics phase (a HIP graph, or eager without
+    """One report at a time: per report the statistics phase (a HIP graph, or eager without
     one) between two timing events, then the rest -- on N GPUs the shard's score partials, the
     eager all_gather and the combine; on 1 GPU the scores graph.  Returns (last result, elapsed
     s between barriers, mean statistics ms or None)."""
@@ -179,11 +179,12 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
     rep = batch.MatrixReporter(R, K_local, cap=cap, thr_rel=THR, thr_ind=THR, device=dev)
     for _ in range(warmup):
         res = rep.report(ns, s_push)
-    if use_graph and not rep.exchange:
-        # 1 GPU: whole-report graphs two in flight (batch.PipelinedReports) -- report i+1 is
+    if use_graph:
+        # reports two in flight (batch.PipelinedReports), each on its own stream -- report i+1 is
         # queued before report i's results are read on the host; every report lands (host
-        # unpack of the results the scores kernel wrote to pinned memory) inside the timed
-        # region, which holds nothing but back-to-back reports
+        # unpack of the results written to pinned memory) inside the timed region, which holds
+        # nothing but back-to-back reports.  N GPUs: per report statistics, the shard's partials
+        # and the combine as graphs, the all_gather of the partials eager between them
         pipe = rep.pipelined(ns, s_push, timing=time_kernel)
         def one():
             pipe.submit()
@@ -210,8 +211,9 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         keep = min(s_push, cap)
         phases = None
         if graph_phases:
-            # the N-GPU launch mode on this one GPU (same reporter, buffers and warm-up rule), so
-            # that a 1 -> N curve can compare like with like
+            # one report at a time (statistics graph between timing events, then the rest; N
+            # GPUs: partials | eager all_gather | combine), same reporter, buffers and warm-up
+            # rule, on every N: a 1 -> N curve of either field compares one launch mode
             g = rep.graph(ns, s_push)
             warm(g.run, max(1, warmup), world)
             res_p, el_p, km_p = phases_loop(rep, ns, s_push, g, steps, world, time_kernel)
@@ -221,14 +223,10 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
                     kern_ms=float(np.mean(ks)) if ks else None,
                     samples=R * K_local * keep, nseg=R * K_local, keep=keep,
                     launch=pipe_label(pipe), phases=phases)
-    # N GPUs: the statistics, the shard's score partials and the combine replay as HIP graphs;
-    # only the all_gather of the partials between them is an eager collective
-    g = rep.graph(ns, s_push) if use_graph else None
-    if g is not None:
-        warm(g.run, max(1, warmup), world)
-    res, elapsed, kern_ms = phases_loop(rep, ns, s_push, g, steps, world, time_kernel)
+    # eager launches (--no-graph), one report at a time
+    res, elapsed, kern_ms = phases_loop(rep, ns, s_push, None, steps, world, time_kernel)
     keep = min(s_push, cap)
-    launch = phases_label(rep, g)
+    launch = phases_label(rep, None)
     return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed, kern_ms=kern_ms,
                 samples=R * K_local * keep, nseg=R * K_local, keep=keep, launch=launch,
                 phases=dict(elapsed=elapsed, kern_ms=kern_ms, launch=launch,
@@ -253,6 +251,9 @@ def gather_labels(label: str, world: int):
 
 def pipe_label(pipe) -> str:
     """The launch label of a batch.PipelinedReports loop."""
+    if pipe.rep.exchange:
+        return ("hip_graph: reports two in flight on two streams "
+                "(statistics | score partials | eager all_gather | combine)")
     if getattr(pipe, "alt", False):
         return "hip_graph: whole reports, two in flight on two streams"
     return "hip_graph: whole reports, two in flight"
@@ -274,47 +275,29 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     rep = batch.MatrixReporter(R, len(kidx), cap=cap, thr_rel=THR, thr_ind=THR, device=dev)
     for _ in range(warmup):
         res = rep.report_records(recs, rec_off)
-    if not rep.exchange:
-        # 1 GPU: whole-report graphs two in flight, as the headline (MatrixReporter.
-        # pipelined_records); the statistics phase timed afterwards on an idle device
-        pipe = rep.pipelined_records(recs, rec_off, timing=True)
-        def one():
-            pipe.submit()
-            pipe.collect()
-        warm(one, max(1, warmup), world)
-        barrier(world)
-        t0 = time.perf_counter()
+    # reports two in flight on two streams, as the headline (MatrixReporter.pipelined_records;
+    # N GPUs: statistics, partials and combine as graphs, the all_gather eager between them); the
+    # statistics phase timed afterwards on an idle device
+    pipe = rep.pipelined_records(recs, rec_off, timing=True)
+    def one():
         pipe.submit()
-        for i in range(steps):
-            if i + 1 < steps:
-                pipe.submit()
-            res, _ = pipe.collect()
-        barrier(world)
-        elapsed = time.perf_counter() - t0
-        ks = []
-        for _ in range(TIMED_REPORTS):
-            pipe.submit(timed=True)
-            ks.append(pipe.collect()[1])
-        stats_ms = float(np.mean(ks))
-        launch = pipe_label(pipe)
-    else:
-        # N GPUs: as the other legs -- statistics, score partials and combine as HIP graphs,
-        # the all_gather of the partials eager between them
-        g = rep.graph_records(recs, rec_off)
-        warm(g.run, max(1, warmup), world)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(steps)]
-        barrier(world)
-        t0 = time.perf_counter()
-        for i in range(steps):
-            ev[i][0].record()
-            g.run_stats()
-            ev[i][1].record()
-            res = g.run_rest()
-        barrier(world)
-        elapsed = time.perf_counter() - t0
-        stats_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-        launch = "hip_graph: statistics | score partials | eager all_gather | combine"
+        pipe.collect()
+    warm(one, max(1, warmup), world)
+    barrier(world)
+    t0 = time.perf_counter()
+    pipe.submit()
+    for i in range(steps):
+        if i + 1 < steps:
+            pipe.submit()
+        res, _ = pipe.collect()
+    barrier(world)
+    elapsed = time.perf_counter() - t0
+    ks = []
+    for _ in range(TIMED_REPORTS):
+        pipe.submit(timed=True)
+        ks.append(pipe.collect()[1])
+    stats_ms = comm_max(float(np.mean(ks)), world, dev)
+    launch = pipe_label(pipe)
     tmax = allreduce(elapsed, torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
     nrec = allreduce(float(R * N), torch.distributed.ReduceOp.SUM if world > 1 else None, world, dev)
     out = dict(ranks=R, kernels=K, records_per_rank=int(counts.sum()), cap=cap,
@@ -471,7 +454,7 @@ def main():
                       if torch.distributed.is_available() and torch.distributed.is_initialized() else 1)
     sec_steps = max(10, args.steps // 2)  # the configs[2] / configs[3] legs
     launch_per_rank = gather_labels(r["launch"], world)
-    # the same workload in the N-GPU launch mode (on N > 1 it IS the timed loop above)
+    # the same workload one report at a time (graph phases), measured after the timed loop
     ph = r["phases"]
     phases = None
     if ph is not None:
@@ -583,8 +566,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup, "warmup_min_ms": WARMUP_MIN_MS,
             "ms_per_step": ms_per_step,
-            # the N-GPU launch mode's time per report on the same workload: on 1 GPU measured
-            # after the pipelined loop, on N GPUs equal to ms_per_step (a like-for-like 1 -> N
+            # the one-report-at-a-time launch mode's time per report on the same workload,
+            # measured after the pipelined loop on every N (a like-for-like 1 -> N
             # curve reads this field; "graph_phases" holds its label and rate)
             "ms_per_step_graph_phases": phases["ms_per_step"] if phases else None,
             "graph_phases": phases,

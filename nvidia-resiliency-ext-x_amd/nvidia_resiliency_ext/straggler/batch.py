@@ -255,8 +255,9 @@ class MatrixReporter:
         return ReportGraph(self, None, 0, stats=lambda: self.compute_stats_records(recs, rec_off))
 
     def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False) -> "PipelinedReports":
-        """Reports replayed two deep (1 GPU): report i+1's device work is queued before report
-        i's results are read on the host, each report landing in its own pinned buffer."""
+        """Reports replayed two deep: report i+1's device work is queued before report i's
+        results are read on the host, each report landing in its own pinned buffer (N GPUs: the
+        partials exchange of each report stays an eager collective, issued in report order)."""
         return PipelinedReports(self, ns, s_push, timing)
 
     def pipelined_records(self, recs: torch.Tensor, rec_off: torch.Tensor,
@@ -391,55 +392,52 @@ TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
 
 class _Slot:
     """The buffers of one report in flight: segment statistics, column reference (+ its f32
-    form), the scores epilogue's completion counter, the record-stream bucketing output.  Slot
-    0 is the reporter's own set; `clean` mirrors MatrixReporter._colref_clean for this slot's
-    column reference."""
+    form), the scores epilogue's completion counter, the record-stream bucketing output, the
+    packed results (+ error word) and, on N GPUs, the shard's partials and their gathered copy.
+    Slot 0 is the reporter's own set; `clean` mirrors MatrixReporter._colref_clean for this
+    slot's column reference."""
+
+    _FIELDS = ("stats", "col_ref", "_ref_f32", "done", "_bucket", "out", "err", "partials", "gathered")
 
     def __init__(self, rep: MatrixReporter, primary: bool):
         self.primary = primary
         if primary:
-            self.stats, self.col_ref, self.ref_f32, self.done = rep.stats, rep.col_ref, rep._ref_f32, rep.done
+            self.vals = [getattr(rep, f, None) for f in _Slot._FIELDS]
             self.clean = rep._colref_clean
         else:
-            self.stats = ops.SegmentStats.empty(rep.R * rep.K, rep.device)
-            self.col_ref = torch.empty_like(rep.col_ref)
-            self.ref_f32 = torch.empty_like(rep._ref_f32)
-            self.done = torch.zeros_like(rep.done)
+            out = torch.zeros_like(rep.out)
+            self.vals = [ops.SegmentStats.empty(rep.R * rep.K, rep.device), torch.empty_like(rep.col_ref),
+                         torch.empty_like(rep._ref_f32), torch.zeros_like(rep.done), None, out,
+                         out[rep._e:rep._e + 4].view(torch.int32), torch.empty_like(rep.partials),
+                         torch.empty_like(rep.gathered) if rep.gathered is not None else None]
             self.clean = False  # uninitialised: its first statistics phase initialises it
-        self.bucket = getattr(rep, "_bucket", None) if primary else None
-
-    _FIELDS = ("stats", "col_ref", "_ref_f32", "done", "_bucket")
-
-    def _mine(self):
-        return (self.stats, self.col_ref, self.ref_f32, self.done, self.bucket)
 
     def bind(self, rep: MatrixReporter):
-        """Context: rep's buffers are this slot's (graph capture bakes them into the kernels)."""
+        """Context: rep's buffers are this slot's (graph capture bakes them into the kernels; the
+        eager exchange reads and writes them)."""
         slot = self
 
         class _Bound:
             def __enter__(self):
-                self.saved = tuple(getattr(rep, f, None) for f in _Slot._FIELDS) + (rep._colref_clean,)
-                for f, v in zip(_Slot._FIELDS, slot._mine()):
+                self.saved = [getattr(rep, f, None) for f in _Slot._FIELDS] + [rep._colref_clean]
+                for f, v in zip(_Slot._FIELDS, slot.vals):
                     setattr(rep, f, v)
                 rep._colref_clean = slot.clean
 
             def __exit__(self, *exc):
-                slot.clean, slot.bucket = rep._colref_clean, getattr(rep, "_bucket", None)
-                for f, v in zip(_Slot._FIELDS, self.saved):
+                slot.clean = rep._colref_clean
+                slot.vals = [getattr(rep, f, None) for f in _Slot._FIELDS]  # a bucket allocated inside
+                restore = slot.vals if slot.primary else self.saved[:-1]
+                for f, v in zip(_Slot._FIELDS, restore):
                     setattr(rep, f, v)
-                if slot.primary:  # the reporter's own set: its state is the slot's
-                    rep._bucket = slot.bucket
-                    rep._colref_clean = slot.clean
-                else:
-                    rep._colref_clean = self.saved[-1]
+                rep._colref_clean = slot.clean if slot.primary else self.saved[-1]
                 return False
 
         return _Bound()
 
 
 class PipelinedReports:
-    """Full reports as HIP graphs, two in flight (1 GPU).  Each report -- column-reference init,
+    """Full reports as HIP graphs, two in flight.  Each report -- column-reference init,
     statistics, scores + straggler masks -- ends with its packed results landing in one of two
     pinned host buffers, so the host can read report i while report i+1 runs: the GPU sees
     back-to-back reports instead of one report per host round trip.
@@ -448,7 +446,11 @@ class PipelinedReports:
     instead of after it (the launch-to-launch transition of one stream); report i's scores wait
     for report i-1's, so the individual history advances in submission order.  The inputs a
     report reads must not change until it is collected (collect() orders the caller's stream
-    after it).  NVRX_PIPE_MODE=whole: one whole-report graph per report on the caller's stream.
+    after it).  N GPUs (exchange): per report the statistics, the shard's partials and the
+    combine (+ result copy) are graphs on the report's stream and the all_gather of the partials
+    is issued eagerly between them, in report order on every rank (the gathered buffers are per
+    report in flight too).  NVRX_PIPE_MODE=whole: one whole-report graph per report on the
+    caller's stream (1 GPU).
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
@@ -458,12 +460,12 @@ class PipelinedReports:
 
     def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int,
                  timing: bool = False, stats=None):
-        if rep.exchange:
-            raise RuntimeError("pipelined reports: 1 GPU (the partials exchange is an eager collective)")
+        self.alt = _PIPE_ALT
+        if rep.exchange and not self.alt:
+            raise RuntimeError("pipelined reports on N GPUs: two streams only (NVRX_PIPE_MODE=whole is 1 GPU)")
         self.rep, self.timing = rep, timing
         if stats is None:
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
-        self.alt = _PIPE_ALT
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
 
         def scores(k: int):
@@ -485,16 +487,28 @@ class PipelinedReports:
                     scores(k)
             return g
 
+        def capture_fn(fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn()
+            return g
+
         if self.alt:
             self.slots = [_Slot(rep, True), _Slot(rep, False)]
-            self.stats_g, self.rest_g = [], []
+            self.stats_g, self.rest_g, self.part_g, self.fin_g = [], [], [], []
             for k, slot in enumerate(self.slots):
                 with slot.bind(rep):
                     _warm_up(rep, stats)  # initialises this slot's column reference too
                     self.stats_g.append(capture(True, False, k))
-                    self.rest_g.append(capture(False, True, k))
+                    if rep.exchange:  # N GPUs: partials | eager all_gather | combine + result copy
+                        self.part_g.append(capture_fn(rep._scores_partials))
+                        self.fin_g.append(capture_fn(lambda k=k: (
+                            rep._finalize(), self.bufs[k].copy_(rep.out, non_blocking=True))))
+                    else:
+                        self.rest_g.append(capture(False, True, k))
             self._needs_clean = rep._colref_clean
             self.streams = [torch.cuda.Stream(rep.device) for _ in range(2)]
+            self.hist_done = [torch.cuda.Event() for _ in range(2)]
         else:
             _warm_up(rep, stats)
             self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
@@ -539,8 +553,18 @@ class PipelinedReports:
                 self.stats_g[k].replay()
                 if timed:
                     self.ev[1].record(s)
-                s.wait_event(self.done[k ^ 1])  # report i-1's scores: the history's order
-                self.rest_g[k].replay()
+                s.wait_event(self.hist_done[k ^ 1])  # report i-1's history update comes first
+                if self.rep.exchange:
+                    self.part_g[k].replay()
+                    self.hist_done[k].record(s)
+                    # the eager all_gather of this slot's partials, ordered after them on s (every
+                    # rank submits its reports, hence its collectives, in the same order)
+                    with self.slots[k].bind(self.rep):
+                        self.rep._exchange()
+                    self.fin_g[k].replay()
+                else:
+                    self.rest_g[k].replay()
+                    self.hist_done[k].record(s)
             self.done[k].record(s)
         else:
             if timed:

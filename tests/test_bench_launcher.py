@@ -66,17 +66,19 @@ def test_launcher_four_ranks_gloo_rehearsal():
     lat, zipf = line["latency_4096_ranks"], line["zipf_16384_ranks"]
     assert lat["straggler_sets_exact"] is True and sum(lat["kernels_per_rank"]) == 2048
     assert zipf["straggler_sets_exact"] is True and sum(zipf["kernels_per_rank"]) == 2048
-    # every rank runs the same launch mode -- statistics, partials and the
-    # combine as graphs, only the all_gather eager -- and the strong-scaled legs report what one
-    # GPU reports (f64 combine order aside)
+    # every rank runs the same launch mode -- reports two in flight, each
+    # one's statistics, partials and combine as graphs, only the all_gather eager -- and the
+    # strong-scaled legs report what one GPU reports (f64 combine order aside)
+    piped = ("hip_graph: reports two in flight on two streams "
+             "(statistics | score partials | eager all_gather | combine)")
+    assert cfg["launch_per_rank"] == [piped] * 4 and lat["launch_per_rank"] == [piped] * 4
+    assert zipf["launch_per_rank"] == [piped] * 4
+    # every point also carries the one-report-at-a-time launch mode's time,
+    # labelled (on N > 1: partials | eager all_gather | combine)
     want = "hip_graph: statistics | score partials | eager all_gather | combine"
-    assert cfg["launch_per_rank"] == [want] * 4 and lat["launch_per_rank"] == [want] * 4
-    assert zipf["launch_per_rank"] == [want] * 4
-    # every point carries the N-GPU launch mode's time, labelled; on N > 1
-    # it is the headline loop itself
     gp = line["graph_phases"]
     assert gp["launch_per_rank"] == [want] * 4 and gp["straggler_sets_exact"] is True
-    assert line["ms_per_step_graph_phases"] == line["ms_per_step"]
+    assert line["ms_per_step_graph_phases"] > 0
     one = _run(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
     pipelined = "hip_graph: whole reports, two in flight on two streams"
     assert one["zipf_16384_ranks"]["launch_per_rank"] == [pipelined]

@@ -153,3 +153,43 @@ def test_unpaired_statistics_replay_is_refused():
     np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
     for res in (g.run(), (pipe.submit(), pipe.collect()[0])[1]):
         np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
+
+
+@pytest.mark.parametrize("records", [False, True])
+def test_two_in_flight_on_two_streams_keep_history_order(records):
+    """Two reports in flight on the two streams (each with its own statistics / reference /
+    bucketing buffers): report i's scores wait for report i-1's, so the individual history --
+    and every score -- equals eager reports in submission order; the inputs change only after
+    the reports reading them were collected."""
+    R, K = 32, 128
+    if records:
+        counts = synth.zipf_counts(K, top=600)
+        slot, occ = synth.zipf_order(counts)
+        t = lambda a: torch.from_numpy(a.view(np.int32)).cuda()  # noqa: E731
+        src = [synth.synth_records(R, t(slot), t(occ), K, int(counts.max()), seed=5 + i) for i in range(2)]
+        off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * slot.size
+        a = batch.MatrixReporter(R, K, cap=256, thr_rel=0.8, thr_ind=0.8)
+        b = batch.MatrixReporter(R, K, cap=256, thr_rel=0.8, thr_ind=0.8)
+        run = lambda x: a.report_records(x, off)  # noqa: E731
+        buf = torch.empty_like(src[0])
+        pipe = b.pipelined_records(buf, off, timing=True)
+    else:
+        S = 700
+        src = [synth.synth_matrix(R, K, S, seed=40 + i, device="cuda") for i in range(2)]
+        a = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
+        b = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
+        run = lambda x: a.report(x, S)  # noqa: E731
+        buf = torch.empty_like(src[0])
+        pipe = b.pipelined(buf, S, timing=True)
+    order = [0, 0, 1, 1, 0, 0, 1, 1]
+    want = [run(src[i]) for i in order]
+    got = []
+    for j in range(0, len(order), 2):
+        buf.copy_(src[order[j]])
+        pipe.submit()
+        pipe.submit(timed=j == 4)
+        got += [pipe.collect()[0], pipe.collect()[0]]
+    for w, g in zip(want, got):
+        np.testing.assert_array_equal(w.gpu_relative, g.gpu_relative)
+        np.testing.assert_array_equal(w.gpu_individual, g.gpu_individual)
+        np.testing.assert_array_equal(w.stragglers_individual, g.stragglers_individual)
