@@ -250,13 +250,13 @@ def gather_labels(label: str, world: int):
 
 
 def pipe_label(pipe) -> str:
-    """The launch label of a batch.PipelinedReports loop."""
+    """The launch label of a batch.PipelinedReports loop (its mode: alt / side / whole)."""
+    base = {"alt": "hip_graph: reports two in flight, each on its own stream",
+            "side": "hip_graph: reports two in flight, statistics | rest on two streams",
+            "whole": "hip_graph: whole reports, two in flight"}[pipe.mode]
     if pipe.rep.exchange:
-        return ("hip_graph: reports two in flight on two streams "
-                "(statistics | score partials | eager all_gather | combine)")
-    if getattr(pipe, "alt", False):
-        return "hip_graph: whole reports, two in flight on two streams"
-    return "hip_graph: whole reports, two in flight"
+        base += " (statistics | score partials | eager all_gather | combine)"
+    return base
 
 
 def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):

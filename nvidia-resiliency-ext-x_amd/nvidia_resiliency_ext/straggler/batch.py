@@ -254,18 +254,19 @@ class MatrixReporter:
         """graph() over record streams resident in HBM (compute_stats_records captured)."""
         return ReportGraph(self, None, 0, stats=lambda: self.compute_stats_records(recs, rec_off))
 
-    def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False) -> "PipelinedReports":
+    def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False,
+                  mode: Optional[str] = None) -> "PipelinedReports":
         """Reports replayed two deep: report i+1's device work is queued before report i's
         results are read on the host, each report landing in its own pinned buffer (N GPUs: the
         partials exchange of each report stays an eager collective, issued in report order)."""
-        return PipelinedReports(self, ns, s_push, timing)
+        return PipelinedReports(self, ns, s_push, timing, mode=mode)
 
     def pipelined_records(self, recs: torch.Tensor, rec_off: torch.Tensor,
-                          timing: bool = False) -> "PipelinedReports":
+                          timing: bool = False, mode: Optional[str] = None) -> "PipelinedReports":
         """pipelined() over record streams resident in HBM (compute_stats_records: bucketing,
         classification and the class kernels -- side-stream fork / join and stream-ordered
         scratch included -- captured into the report graphs)."""
-        return PipelinedReports(self, None, 0, timing,
+        return PipelinedReports(self, None, 0, timing, mode=mode, stats_bytes=8 * recs.shape[0],
                                 stats=lambda: self.compute_stats_records(recs, rec_off))
 
     def _unpack(self, buf: Optional[torch.Tensor] = None) -> BatchResult:
@@ -383,9 +384,17 @@ def _warm_up(rep: MatrixReporter, stats) -> None:
 # NVRX_PIPE_D2H=copy: pipelined reports write a device buffer and copy it to the pinned one
 # (one more graph node) instead of the scores kernel writing pinned host memory directly
 _PIPE_COPY = os.environ.get("NVRX_PIPE_D2H", "") == "copy"
-# NVRX_PIPE_MODE=whole: pipelined reports as whole-report graphs on one stream (round 4) instead
-# of each report on its own stream of two (timing A/B)
-_PIPE_ALT = os.environ.get("NVRX_PIPE_MODE", "alt") != "whole"
+# NVRX_PIPE_MODE (timing A/B; PipelinedReports(mode=...) overrides the default, "auto"): "alt" each
+# report on its own stream of two; "side" the statistics phases on one stream, the rest of every
+# report on another; "whole" one whole-report graph per report on the caller's stream (round 4)
+_PIPE_MODE = os.environ.get("NVRX_PIPE_MODE", "")
+# "auto": alt while a report's statistics phase reads at most this many bytes.  Two reports'
+# statistics kernels then overlap at their launch boundaries (one launch's ramp and tail, ~15-35
+# us) -- configs[1] (4.3 GB) 0.675-0.687 -> 0.653-0.684 ms per report by box; a longer phase gains
+# nothing there and loses to the two kernels sharing the GPU for their whole duration: configs[2]
+# (34 GB) 5.57 ms whole, 5.65 side, 5.79 alt (profiles/r05/pipe_modes.json).  Above it: whole on 1
+# GPU, side on N GPUs (the exchange sits between a report's phases, so it needs two streams).
+PIPE_ALT_MAX_BYTES = 8 << 30
 
 TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
 
@@ -441,16 +450,18 @@ class PipelinedReports:
     statistics, scores + straggler masks -- ends with its packed results landing in one of two
     pinned host buffers, so the host can read report i while report i+1 runs: the GPU sees
     back-to-back reports instead of one report per host round trip.
-    Two streams (default): report i runs on stream i % 2 with its own set of statistics /
-    reference buffers (_Slot), so report i+1's statistics kernel starts while report i's drains
-    instead of after it (the launch-to-launch transition of one stream); report i's scores wait
-    for report i-1's, so the individual history advances in submission order.  The inputs a
-    report reads must not change until it is collected (collect() orders the caller's stream
-    after it).  N GPUs (exchange): per report the statistics, the shard's partials and the
-    combine (+ result copy) are graphs on the report's stream and the all_gather of the partials
-    is issued eagerly between them, in report order on every rank (the gathered buffers are per
-    report in flight too).  NVRX_PIPE_MODE=whole: one whole-report graph per report on the
-    caller's stream (1 GPU).
+    mode "alt": report i runs on stream i % 2 with its own set of statistics / reference
+    buffers (_Slot), so report i+1's statistics kernel starts while report i's drains instead of
+    after it (the launch-to-launch transition of one stream); report i's scores wait for report
+    i-1's, so the individual history advances in submission order.  "side": every statistics
+    phase on one stream, every rest on another (buffer sets per report in flight as in alt).
+    "whole": one whole-report graph per report on the caller's stream (1 GPU).  "auto" (default):
+    alt for statistics phases up to PIPE_ALT_MAX_BYTES, else whole (side on N GPUs).  With two
+    streams the inputs a report reads must not change until it is collected (collect() orders
+    the caller's stream after it).  N GPUs (exchange): per report the statistics, the shard's
+    partials and the combine (+ result copy) are graphs and the all_gather of the partials is
+    issued eagerly between them, in report order on every rank (the gathered buffers are per
+    report in flight too).
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
@@ -459,10 +470,25 @@ class PipelinedReports:
     streams: MatrixReporter.pipelined_records)."""
 
     def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int,
-                 timing: bool = False, stats=None):
-        self.alt = _PIPE_ALT
-        if rep.exchange and not self.alt:
-            raise RuntimeError("pipelined reports on N GPUs: two streams only (NVRX_PIPE_MODE=whole is 1 GPU)")
+                 timing: bool = False, stats=None, mode: Optional[str] = None,
+                 stats_bytes: Optional[int] = None):
+        self.mode = mode or _PIPE_MODE or "auto"
+        if self.mode == "auto":
+            if stats_bytes is None:  # the matrix path: 4 B per retained sample
+                keep = min(s_push, rep.cap) if rep.cap > 0 else s_push
+                stats_bytes = 4 * rep.R * rep.K * keep
+            if rep.exchange and rep.world > 1:  # one mode on every rank (shards differ in size)
+                x = torch.tensor([float(stats_bytes)], dtype=torch.float64,
+                                 device="cpu" if rep.gloo else rep.device)
+                torch.distributed.all_reduce(x, torch.distributed.ReduceOp.MAX, group=rep.group)
+                stats_bytes = int(x.item())
+            self.mode = ("alt" if stats_bytes <= PIPE_ALT_MAX_BYTES else
+                         "side" if rep.exchange else "whole")
+        if self.mode not in ("alt", "side", "whole"):
+            raise ValueError(f"pipelined reports: mode {self.mode!r} (auto | alt | side | whole)")
+        if rep.exchange and self.mode == "whole":
+            raise RuntimeError("pipelined reports on N GPUs: two streams only (mode 'whole' is 1 GPU)")
+        self.alt = self.mode != "whole"  # two streams, a buffer set per report in flight
         self.rep, self.timing = rep, timing
         if stats is None:
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
@@ -509,6 +535,7 @@ class PipelinedReports:
             self._needs_clean = rep._colref_clean
             self.streams = [torch.cuda.Stream(rep.device) for _ in range(2)]
             self.hist_done = [torch.cuda.Event() for _ in range(2)]
+            self.stats_done = [torch.cuda.Event() for _ in range(2)]
         else:
             _warm_up(rep, stats)
             self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
@@ -543,16 +570,23 @@ class PipelinedReports:
             if spin is not None:
                 spin(TIMED_SPIN_CYCLES)
         if self.alt:
-            s = self.streams[k]
-            # the caller's work so far (inputs; the wait for the collected reports) comes first;
-            # slot k's previous report ran on this stream
+            # alt: report i on stream i % 2; side: every statistics phase on stream 0, every rest
+            # on stream 1 (slot k's previous report has finished with its buffers: done[k])
+            s = self.streams[k] if self.mode == "alt" else self.streams[0]
+            # the caller's work so far (inputs; the wait for the collected reports) comes first
             s.wait_stream(torch.cuda.current_stream(self.rep.device))
+            s.wait_event(self.done[k])
             with torch.cuda.stream(s):
                 if timed:
                     self.ev[0].record(s)
                 self.stats_g[k].replay()
                 if timed:
                     self.ev[1].record(s)
+            if self.mode == "side":
+                self.stats_done[k].record(s)
+                s = self.streams[1]
+                s.wait_event(self.stats_done[k])
+            with torch.cuda.stream(s):
                 s.wait_event(self.hist_done[k ^ 1])  # report i-1's history update comes first
                 if self.rep.exchange:
                     self.part_g[k].replay()

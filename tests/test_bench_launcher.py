@@ -69,10 +69,13 @@ def test_launcher_four_ranks_gloo_rehearsal():
     # every rank runs the same launch mode -- reports two in flight, each
     # one's statistics, partials and combine as graphs, only the all_gather eager -- and the
     # strong-scaled legs report what one GPU reports (f64 combine order aside)
-    piped = ("hip_graph: reports two in flight on two streams "
-             "(statistics | score partials | eager all_gather | combine)")
-    assert cfg["launch_per_rank"] == [piped] * 4 and lat["launch_per_rank"] == [piped] * 4
-    assert zipf["launch_per_rank"] == [piped] * 4
+    for leg in (cfg, lat, zipf):
+        labels = leg["launch_per_rank"]
+        assert len(labels) == 4 and len(set(labels)) == 1, labels
+        assert labels[0].startswith("hip_graph: reports two in flight"), labels
+        assert labels[0].endswith("(statistics | score partials | eager all_gather | combine)"), labels
+    # configs[1] per GPU (4.3 GB of samples per report): each report on its own stream
+    assert cfg["launch_per_rank"][0].startswith("hip_graph: reports two in flight, each on its own stream")
     # every point also carries the one-report-at-a-time launch mode's time,
     # labelled (on N > 1: partials | eager all_gather | combine)
     want = "hip_graph: statistics | score partials | eager all_gather | combine"
@@ -80,9 +83,10 @@ def test_launcher_four_ranks_gloo_rehearsal():
     assert gp["launch_per_rank"] == [want] * 4 and gp["straggler_sets_exact"] is True
     assert line["ms_per_step_graph_phases"] > 0
     one = _run(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], timeout=580)
-    pipelined = "hip_graph: whole reports, two in flight on two streams"
-    assert one["zipf_16384_ranks"]["launch_per_rank"] == [pipelined]
-    assert one["config"]["launch"] == pipelined
+    alt = "hip_graph: reports two in flight, each on its own stream"
+    assert one["zipf_16384_ranks"]["launch_per_rank"] == [alt] and one["config"]["launch"] == alt
+    # configs[2] (34 GB of samples per report): whole reports on one stream (PIPE_ALT_MAX_BYTES)
+    assert one["latency_4096_ranks"]["launch_per_rank"] == ["hip_graph: whole reports, two in flight"]
     assert one["graph_phases"]["launch_per_rank"] == ["hip_graph: statistics | rest"]
     assert one["graph_phases"]["straggler_sets_exact"] is True
     assert one["ms_per_step_graph_phases"] > 0

@@ -155,8 +155,9 @@ def test_unpaired_statistics_replay_is_refused():
         np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
 
 
+@pytest.mark.parametrize("mode", ["alt", "side", "whole"])
 @pytest.mark.parametrize("records", [False, True])
-def test_two_in_flight_on_two_streams_keep_history_order(records):
+def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
     """Two reports in flight on the two streams (each with its own statistics / reference /
     bucketing buffers): report i's scores wait for report i-1's, so the individual history --
     and every score -- equals eager reports in submission order; the inputs change only after
@@ -172,7 +173,7 @@ def test_two_in_flight_on_two_streams_keep_history_order(records):
         b = batch.MatrixReporter(R, K, cap=256, thr_rel=0.8, thr_ind=0.8)
         run = lambda x: a.report_records(x, off)  # noqa: E731
         buf = torch.empty_like(src[0])
-        pipe = b.pipelined_records(buf, off, timing=True)
+        pipe = b.pipelined_records(buf, off, timing=True, mode=mode)
     else:
         S = 700
         src = [synth.synth_matrix(R, K, S, seed=40 + i, device="cuda") for i in range(2)]
@@ -180,7 +181,7 @@ def test_two_in_flight_on_two_streams_keep_history_order(records):
         b = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
         run = lambda x: a.report(x, S)  # noqa: E731
         buf = torch.empty_like(src[0])
-        pipe = b.pipelined(buf, S, timing=True)
+        pipe = b.pipelined(buf, S, timing=True, mode=mode)
     order = [0, 0, 1, 1, 0, 0, 1, 1]
     want = [run(src[i]) for i in order]
     got = []

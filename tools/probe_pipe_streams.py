@@ -1,7 +1,9 @@
-"""configs[1] pipelined reports, two streams (batch.PipelinedReports default) against whole-report
-graphs on one stream (NVRX_PIPE_MODE=whole), interleaved in one
-process (the box's clock drift cancels): ROUNDS x (N reports of each mode), ms per report of
-each block, then the medians.  Usage: python tools/probe_pipe_streams.py [N] [ROUNDS]."""
+"""Pipelined reports by launch mode (batch.PipelinedReports: alt = each report on its own stream of
+two, side = statistics on one stream and the rest on another, whole = one whole-report graph per
+report on one stream), interleaved in one process so the box's clock drift cancels: ROUNDS x (N
+reports of each mode), ms per report of each block, then the medians.
+Usage: python tools/probe_pipe_streams.py [N] [ROUNDS] [config: c1 | c2]  (c1 = configs[1]
+64 x 2048 x 10000 pushed, c2 = configs[2] 4096 x 2048 x 1024)."""
 import json
 import os
 import sys
@@ -14,15 +16,14 @@ import torch  # noqa: E402
 
 from nvidia_resiliency_ext.straggler import batch, synth  # noqa: E402
 
-R, K, S, CAP = 64, 2048, 10000, 8192
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 ROUNDS = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+CFG = sys.argv[3] if len(sys.argv) > 3 else "c1"
+R, K, S, CAP = (64, 2048, 10000, 8192) if CFG == "c1" else (4096, 2048, 1024, 8192)
+MODES = os.environ.get("MODES", "alt,side,whole").split(",")
 ns = synth.synth_matrix(R, K, S, device="cuda")
 rep = batch.MatrixReporter(R, K, cap=CAP, thr_rel=0.8, thr_ind=0.8)
-pipes = {}
-for name, alt in (("two_streams", True), ("whole", False)):
-    batch._PIPE_ALT = alt
-    pipes[name] = rep.pipelined(ns, S)
+pipes = {m: rep.pipelined(ns, S, mode=m) for m in MODES}
 
 
 def block(p, n):
@@ -37,9 +38,11 @@ def block(p, n):
 
 out = {k: [] for k in pipes}
 for k, p in pipes.items():
-    block(p, 100)  # warm
+    block(p, max(4, N // 3))  # warm
 for r in range(ROUNDS):
-    for k, p in (list(pipes.items()) if r % 2 == 0 else list(reversed(list(pipes.items())))):
+    items = list(pipes.items())
+    for k, p in (items if r % 2 == 0 else items[::-1]):
         out[k].append(block(p, N))
         print(k, round(out[k][-1], 4), flush=True)
-print("RESULT " + json.dumps({k: dict(median_ms=float(np.median(v)), runs=v) for k, v in out.items()}))
+print("RESULT " + json.dumps({"config": CFG, **{k: dict(median_ms=float(np.median(v)), runs=v)
+                                                for k, v in out.items()}}))
