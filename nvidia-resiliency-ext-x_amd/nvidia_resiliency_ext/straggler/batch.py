@@ -255,11 +255,11 @@ class MatrixReporter:
         return ReportGraph(self, None, 0, stats=lambda: self.compute_stats_records(recs, rec_off))
 
     def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False,
-                  mode: Optional[str] = None) -> "PipelinedReports":
+                  mode: Optional[str] = None, depth: int = 2) -> "PipelinedReports":
         """Reports replayed two deep: report i+1's device work is queued before report i's
         results are read on the host, each report landing in its own pinned buffer (N GPUs: the
         partials exchange of each report stays an eager collective, issued in report order)."""
-        return PipelinedReports(self, ns, s_push, timing, mode=mode)
+        return PipelinedReports(self, ns, s_push, timing, mode=mode, depth=depth)
 
     def pipelined_records(self, recs: torch.Tensor, rec_off: torch.Tensor,
                           timing: bool = False, mode: Optional[str] = None) -> "PipelinedReports":
@@ -471,7 +471,7 @@ class PipelinedReports:
 
     def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int,
                  timing: bool = False, stats=None, mode: Optional[str] = None,
-                 stats_bytes: Optional[int] = None):
+                 stats_bytes: Optional[int] = None, depth: int = 2):
         self.mode = mode or _PIPE_MODE or "auto"
         if self.mode == "auto":
             if stats_bytes is None:  # the matrix path: 4 B per retained sample
@@ -489,10 +489,13 @@ class PipelinedReports:
         if rep.exchange and self.mode == "whole":
             raise RuntimeError("pipelined reports on N GPUs: two streams only (mode 'whole' is 1 GPU)")
         self.alt = self.mode != "whole"  # two streams, a buffer set per report in flight
+        if depth < 2 or (depth > 2 and not self.alt):
+            raise ValueError("pipelined reports: depth >= 2 (> 2 with two streams only)")
+        self.depth = depth
         self.rep, self.timing = rep, timing
         if stats is None:
             stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
-        self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(2)]
+        self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(depth)]
 
         def scores(k: int):
             # the scores kernel writes the pinned buffer itself when its epilogue stores the
@@ -520,7 +523,7 @@ class PipelinedReports:
             return g
 
         if self.alt:
-            self.slots = [_Slot(rep, True), _Slot(rep, False)]
+            self.slots = [_Slot(rep, True)] + [_Slot(rep, False) for _ in range(depth - 1)]
             self.stats_g, self.rest_g, self.part_g, self.fin_g = [], [], [], []
             for k, slot in enumerate(self.slots):
                 with slot.bind(rep):
@@ -533,9 +536,9 @@ class PipelinedReports:
                     else:
                         self.rest_g.append(capture(False, True, k))
             self._needs_clean = rep._colref_clean
-            self.streams = [torch.cuda.Stream(rep.device) for _ in range(2)]
-            self.hist_done = [torch.cuda.Event() for _ in range(2)]
-            self.stats_done = [torch.cuda.Event() for _ in range(2)]
+            self.streams = [torch.cuda.Stream(rep.device) for _ in range(depth)]
+            self.hist_done = [torch.cuda.Event() for _ in range(depth)]
+            self.stats_done = [torch.cuda.Event() for _ in range(depth)]
         else:
             _warm_up(rep, stats)
             self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
@@ -545,21 +548,21 @@ class PipelinedReports:
                 self.rest = [capture(False, True, k) for k in range(2)]
         if timing:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        self.done = [torch.cuda.Event() for _ in range(2)]
+        self.done = [torch.cuda.Event() for _ in range(depth)]
         self.pending = []  # (slot, timed) in flight, oldest first
         self.ready = []    # results collected early (a timed submit drains), oldest first
         self.n = 0
 
     def submit(self, timed: bool = False) -> None:
         """Queue the next report (at most two in flight: collect() the oldest first)."""
-        if len(self.pending) == 2:
-            raise RuntimeError("two reports in flight: collect() one first")
+        if len(self.pending) == self.depth:
+            raise RuntimeError(f"{self.depth} reports in flight: collect() one first")
         if self._needs_clean and not self.rep._colref_clean:
             raise RuntimeError("PipelinedReports: an unpaired statistics phase (ReportGraph."
                                "run_stats without run_rest) left the column reference in use")
         if timed and not self.timing:
             raise RuntimeError("PipelinedReports(timing=True) is needed for timed reports")
-        k = self.n & 1
+        k = self.n % self.depth
         if timed:
             while self.pending:  # the device idles before the measured statistics phase
                 self.ready.append(self._land())
@@ -587,7 +590,7 @@ class PipelinedReports:
                 s = self.streams[1]
                 s.wait_event(self.stats_done[k])
             with torch.cuda.stream(s):
-                s.wait_event(self.hist_done[k ^ 1])  # report i-1's history update comes first
+                s.wait_event(self.hist_done[(k - 1) % self.depth])  # report i-1's history update first
                 if self.rep.exchange:
                     self.part_g[k].replay()
                     self.hist_done[k].record(s)

@@ -23,14 +23,18 @@ R, K, S, CAP = (64, 2048, 10000, 8192) if CFG == "c1" else (4096, 2048, 1024, 81
 MODES = os.environ.get("MODES", "alt,side,whole").split(",")
 ns = synth.synth_matrix(R, K, S, device="cuda")
 rep = batch.MatrixReporter(R, K, cap=CAP, thr_rel=0.8, thr_ind=0.8)
-pipes = {m: rep.pipelined(ns, S, mode=m) for m in MODES}
+# a mode name may end in the pipeline depth (alt3: three reports in flight on three streams)
+pipes = {m: rep.pipelined(ns, S, mode=m.rstrip("0123456789"), depth=int(m[len(m.rstrip("0123456789")):] or 2))
+         for m in MODES}
 
 
 def block(p, n):
-    p.submit()
+    d = p.depth
+    for _ in range(d - 1):
+        p.submit()
     t0 = time.perf_counter()
     for i in range(n):
-        if i + 1 < n:
+        if i + d - 1 < n:
             p.submit()
         p.collect()
     return (time.perf_counter() - t0) / n * 1e3
