@@ -131,6 +131,20 @@ def warm(step, n_min: int, world: int) -> int:
     return n
 
 
+def warm_pipelined(pipe, warmup: int, world: int) -> int:
+    """The untimed warm-up of a pipelined loop in its own pattern (two reports in flight, report
+    i+1 queued before report i is collected), at least `warmup` reports and WARMUP_MIN_MS (warm());
+    drained at the end, so the timed region starts from an empty pipeline."""
+    pipe.submit()
+
+    def one():
+        pipe.submit()
+        pipe.collect()
+    n = warm(one, max(1, warmup), world)
+    pipe.collect()
+    return n
+
+
 def phases_loop(rep, ns, s_push, g, steps, world, time_kernel):
     """One report at a time: per report the statistics phase (a HIP graph, or eager without
     one) between two timing events, then the rest -- on N GPUs the shard's score partials, the
@@ -186,10 +200,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         # nothing but back-to-back reports.  N GPUs: per report statistics, the shard's partials
         # and the combine as graphs, the all_gather of the partials eager between them
         pipe = rep.pipelined(ns, s_push, timing=time_kernel)
-        def one():
-            pipe.submit()
-            pipe.collect()
-        warm(one, max(1, warmup), world)
+        warm_pipelined(pipe, warmup, world)
         barrier(world)
         t0 = time.perf_counter()
         pipe.submit()
@@ -279,10 +290,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     # N GPUs: statistics, partials and combine as graphs, the all_gather eager between them); the
     # statistics phase timed afterwards on an idle device
     pipe = rep.pipelined_records(recs, rec_off, timing=True)
-    def one():
-        pipe.submit()
-        pipe.collect()
-    warm(one, max(1, warmup), world)
+    warm_pipelined(pipe, warmup, world)
     barrier(world)
     t0 = time.perf_counter()
     pipe.submit()

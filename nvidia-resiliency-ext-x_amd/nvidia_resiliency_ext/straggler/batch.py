@@ -397,6 +397,14 @@ _PIPE_MODE = os.environ.get("NVRX_PIPE_MODE", "")
 PIPE_ALT_MAX_BYTES = 8 << 30
 
 TIMED_SPIN_CYCLES = 50_000  # ~20-25 us of device spin ahead of a timed report
+STAGGER_FRAC = 0.25  # PipelinedReports: a burst's second report starts this much of a phase later
+
+
+def _spin(cycles: int) -> None:
+    """A one-wave device spin on the current stream (torch's private _sleep kernel)."""
+    spin = getattr(torch.cuda, "_sleep", None)
+    if spin is not None:
+        spin(int(cycles))
 
 
 class _Slot:
@@ -473,10 +481,10 @@ class PipelinedReports:
                  timing: bool = False, stats=None, mode: Optional[str] = None,
                  stats_bytes: Optional[int] = None, depth: int = 2):
         self.mode = mode or _PIPE_MODE or "auto"
+        if stats_bytes is None:  # the matrix path: 4 B per retained sample
+            keep = min(s_push, rep.cap) if rep.cap > 0 else s_push
+            stats_bytes = 4 * rep.R * rep.K * keep
         if self.mode == "auto":
-            if stats_bytes is None:  # the matrix path: 4 B per retained sample
-                keep = min(s_push, rep.cap) if rep.cap > 0 else s_push
-                stats_bytes = 4 * rep.R * rep.K * keep
             if rep.exchange and rep.world > 1:  # one mode on every rank (shards differ in size)
                 x = torch.tensor([float(stats_bytes)], dtype=torch.float64,
                                  device="cpu" if rep.gloo else rep.device)
@@ -549,6 +557,11 @@ class PipelinedReports:
         if timing:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         self.done = [torch.cuda.Event() for _ in range(depth)]
+        # the one-time stagger of a burst's second report: a quarter of the statistics phase at
+        # ~6.5 TB/s (STAGGER_FRAC; NVRX_PIPE_STAGGER=0 disables), in spin cycles of ~2.2 GHz
+        frac = float(os.environ.get("NVRX_PIPE_STAGGER", STAGGER_FRAC))
+        self.stagger_cycles = int(frac * stats_bytes / 6.5e12 * 2.2e9) if stats_bytes else 0
+        self._burst = -2
         self.pending = []  # (slot, timed) in flight, oldest first
         self.ready = []    # results collected early (a timed submit drains), oldest first
         self.n = 0
@@ -579,14 +592,27 @@ class PipelinedReports:
             # the caller's work so far (inputs; the wait for the collected reports) comes first
             s.wait_stream(torch.cuda.current_stream(self.rep.device))
             s.wait_event(self.done[k])
+            if self.mode == "alt" and self.depth > 2:
+                # at most two statistics phases at once: report i's starts on the device as soon
+                # as report i-2's has finished, with no host round trip in between
+                s.wait_event(self.stats_done[(k - 2) % self.depth])
+            if (self.mode == "alt" and self.stagger_cycles > 0 and len(self.pending) == 1
+                    and self.n == self._burst + 1):
+                # the second report of a burst (the pipeline was empty when the first was
+                # submitted) starts a quarter of a statistics phase after the first: staggered,
+                # one report's statistics kernel covers the other's end, scores and the host's
+                # next submission; started together, the two stay locked and the device idles at
+                # every pair's end
+                with torch.cuda.stream(s):
+                    _spin(self.stagger_cycles)
             with torch.cuda.stream(s):
                 if timed:
                     self.ev[0].record(s)
                 self.stats_g[k].replay()
                 if timed:
                     self.ev[1].record(s)
+            self.stats_done[k].record(s)
             if self.mode == "side":
-                self.stats_done[k].record(s)
                 s = self.streams[1]
                 s.wait_event(self.stats_done[k])
             with torch.cuda.stream(s):
@@ -613,6 +639,8 @@ class PipelinedReports:
                 self.full[k].replay()
             self.done[k].record()
         self.rep._colref_clean = self.rep._fuse_ref()
+        if not self.pending:
+            self._burst = self.n  # the first report of a burst (submitted to an empty pipeline)
         self.pending.append((k, timed))
         self.n += 1
 
