@@ -602,7 +602,11 @@ def main():
                          "alg_bytes_per_launch": alg_bytes,
                          # the same bytes over the pipelined loop's time per report (two reports'
                          # statistics kernels overlap at their boundaries)
-                         "per_report_frac": alg_bytes / (ms_per_step * 1e-3) / HBM_PEAK},
+                         "per_report_frac": alg_bytes / (ms_per_step * 1e-3) / HBM_PEAK,
+                         "kernel_ms_is": "the statistics kernel timed alone on an idle device (HIP "
+                                         "events, after the loop); in the loop two reports' kernels "
+                                         "overlap at their launch boundaries, so ms_per_step can be "
+                                         "below it"},
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,
             "configs0_report": c1,
