@@ -75,20 +75,21 @@ ns2 = synth.synth_matrix(R, K, S, seed=77, device="cuda")
 ref = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8, exchange=False)
 src = [ns, ns, ns2, ns2, ns, ns]  # two reports in flight per input
 want = [ref.report(x, S) for x in src]
-xp = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8, exchange=True)
-buf = torch.empty_like(ns)
-pipe = xp.pipelined(buf, S, timing=True)
-got = []
-for i in range(0, 6, 2):
-    # the input changes only once the reports reading it have been collected
-    buf.copy_(src[i])
-    pipe.submit()
-    pipe.submit(timed=i == 2)  # a timed submit drains the report in flight first
-    got += [pipe.collect()[0], pipe.collect()[0]]
 piped = []
-for a, b in zip(want, got):
-    errs += [maxrel(b.gpu_relative, a.gpu_relative), maxrel(b.gpu_individual, a.gpu_individual)]
-    piped.append(same(a, b))
+for mode in ("alt", "side"):  # each report on its own stream / statistics | rest on two streams
+    xp = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8, exchange=True)
+    buf = torch.empty_like(ns)
+    pipe = xp.pipelined(buf, S, timing=True, mode=mode)
+    got = []
+    for i in range(0, 6, 2):
+        # the input changes only once the reports reading it have been collected
+        buf.copy_(src[i])
+        pipe.submit()
+        pipe.submit(timed=i == 2)  # a timed submit drains the report in flight first
+        got += [pipe.collect()[0], pipe.collect()[0]]
+    for a, b in zip(want, got):
+        errs += [maxrel(b.gpu_relative, a.gpu_relative), maxrel(b.gpu_individual, a.gpu_individual)]
+        piped.append(same(a, b))
 out.update(errs=errs, sets=sets, piped=piped, nrel=int(xz.stragglers_relative.sum()))
 torch.distributed.destroy_process_group()
 print("RESULT " + json.dumps(out))
@@ -103,7 +104,7 @@ def test_rccl_exchange_matches_fused_scoring():
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][7:])
     assert out["backend"] == "nccl"
     assert all(out["sets"]), out
-    assert len(out["piped"]) == 6 and all(out["piped"]), out
+    assert len(out["piped"]) == 12 and all(out["piped"]), out
     # one shard: the finalize kernel divides the same two sums the fused kernel does
     assert max(out["errs"]) <= 1e-13, out["errs"]
     assert out["nrel"] > 0  # the injected straggler ranks are flagged through the exchange
