@@ -479,7 +479,7 @@ def main():
         del r["ns"]
         torch.cuda.empty_cache()
         r4 = run_config(C3, C3["K"], sec_steps, 3, world, rank, dev, time_kernel=True,
-                        use_graph=not args.no_graph)
+                        use_graph=not args.no_graph, graph_phases=not args.no_graph)
         t4 = allreduce(r4["elapsed"], torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)
         tot4 = allreduce(float(r4["samples"]), torch.distributed.ReduceOp.SUM if world > 1 else None,
                          world, dev)
@@ -491,6 +491,10 @@ def main():
                    ms_per_report=t4 / n4 * 1e3, samples_per_s=tot4 * n4 / t4,
                    stats_kernel_ms=k4,
                    stats_kernel_hbm_frac=(4 * r4["samples"] + 24 * r4["nseg"]) / (k4 * 1e-3) / HBM_PEAK,
+                   # one report at a time (samples resident -> scores + sets on the host): the
+                   # latency itself; ms_per_report above is the pipelined rate
+                   latency_ms_one_report=(comm_max(r4["phases"]["elapsed"], world, dev) / n4 * 1e3
+                                          if r4.get("phases") else None),
                    steps=n4, kernels_per_rank=shard_sizes(C3["K"], world),
                    straggler_sets_exact=all_ranks(bool(np.array_equal(
                        s4.stragglers_relative, synth.straggler_ranks(C3["R"]).astype(bool))), world, dev))
