@@ -390,7 +390,8 @@ _PIPE_COPY = os.environ.get("NVRX_PIPE_D2H", "") == "copy"
 _PIPE_MODE = os.environ.get("NVRX_PIPE_MODE", "")
 # "auto": alt while a report's statistics phase reads at most this many bytes.  Two reports'
 # statistics kernels then overlap at their launch boundaries (one launch's ramp and tail, ~15-35
-# us) -- configs[1] (4.3 GB) 0.675-0.687 -> 0.653-0.684 ms per report by box; a longer phase gains
+# us) -- configs[1] (4.3 GB) 0.673-0.687 -> 0.638-0.651 ms per report (with the stagger below,
+# profiles/r05/pipe_modes.json); a longer phase gains
 # nothing there and loses to the two kernels sharing the GPU for their whole duration: configs[2]
 # (34 GB) 5.57 ms whole, 5.65 side, 5.79 alt (profiles/r05/pipe_modes.json).  Above it: whole on 1
 # GPU, side on N GPUs (the exchange sits between a report's phases, so it needs two streams).
@@ -567,7 +568,7 @@ class PipelinedReports:
         self.n = 0
 
     def submit(self, timed: bool = False) -> None:
-        """Queue the next report (at most two in flight: collect() the oldest first)."""
+        """Queue the next report (at most `depth` in flight: collect() the oldest first)."""
         if len(self.pending) == self.depth:
             raise RuntimeError(f"{self.depth} reports in flight: collect() one first")
         if self._needs_clean and not self.rep._colref_clean:
