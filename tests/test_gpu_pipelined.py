@@ -155,7 +155,7 @@ def test_unpaired_statistics_replay_is_refused():
         np.testing.assert_array_equal(res.stragglers_relative, want.stragglers_relative)
 
 
-@pytest.mark.parametrize("mode", ["alt", "side", "whole"])
+@pytest.mark.parametrize("mode", ["alt", "side", "whole", "alt3"])
 @pytest.mark.parametrize("records", [False, True])
 def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
     """Two reports in flight on the two streams (each with its own statistics / reference /
@@ -163,6 +163,8 @@ def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
     and every score -- equals eager reports in submission order; the inputs change only after
     the reports reading them were collected."""
     R, K = 32, 128
+    depth = 3 if mode == "alt3" else 2  # alt3: three reports in flight, two statistics at once
+    mode = mode.rstrip("3")
     if records:
         counts = synth.zipf_counts(K, top=600)
         slot, occ = synth.zipf_order(counts)
@@ -173,7 +175,10 @@ def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
         b = batch.MatrixReporter(R, K, cap=256, thr_rel=0.8, thr_ind=0.8)
         run = lambda x: a.report_records(x, off)  # noqa: E731
         buf = torch.empty_like(src[0])
-        pipe = b.pipelined_records(buf, off, timing=True, mode=mode)
+        # (pipelined_records has no depth argument: PipelinedReports directly, as it builds it)
+        pipe = batch.PipelinedReports(b, None, 0, timing=True, mode=mode, depth=depth,
+                                      stats_bytes=8 * buf.shape[0],
+                                      stats=lambda: b.compute_stats_records(buf, off))
     else:
         S = 700
         src = [synth.synth_matrix(R, K, S, seed=40 + i, device="cuda") for i in range(2)]
@@ -181,7 +186,7 @@ def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
         b = batch.MatrixReporter(R, K, cap=512, thr_rel=0.8, thr_ind=0.8)
         run = lambda x: a.report(x, S)  # noqa: E731
         buf = torch.empty_like(src[0])
-        pipe = b.pipelined(buf, S, timing=True, mode=mode)
+        pipe = b.pipelined(buf, S, timing=True, mode=mode, depth=depth)
     order = [0, 0, 1, 1, 0, 0, 1, 1]
     want = [run(src[i]) for i in order]
     got = []
@@ -190,6 +195,13 @@ def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
         pipe.submit()
         pipe.submit(timed=j == 4)
         got += [pipe.collect()[0], pipe.collect()[0]]
+    if depth > 2:  # three in flight over one input
+        buf.copy_(src[0])
+        want3 = [run(src[0]) for _ in range(3)]
+        for _ in range(3):
+            pipe.submit()
+        got3 = [pipe.collect()[0] for _ in range(3)]
+        want, got = want + want3, got + got3
     for w, g in zip(want, got):
         np.testing.assert_array_equal(w.gpu_relative, g.gpu_relative)
         np.testing.assert_array_equal(w.gpu_individual, g.gpu_individual)
