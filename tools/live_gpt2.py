@@ -1,5 +1,6 @@
-"""configs[4] -- live capture: rocprofiler-sdk kernel-dispatch records from a GPT-2 small DDP
-training loop feeding the on-GPU Reporter (Detector) of this package.
+"""configs[4] -- live capture: kernel-dispatch records (queue delivery by default,
+NVRX_CAPTURE_DELIVERY selects rocprofiler-sdk tracing) from a GPT-2 small DDP training loop
+feeding the on-GPU Reporter (Detector) of this package.
 
 One process per GPU (torchrun; WORLD_SIZE=1 runs plain DDP on one GPU).  GPT-2 small
 (12 layers, d=768, 12 heads, vocab 50257, ctx 1024; random init, synthetic tokens -- there is
@@ -222,6 +223,11 @@ def main():
                  med=np.array([ks[n][S.MED] for n in knames], np.float32),
                  avg=np.array([ks[n][S.AVG] for n in knames], np.float32),
                  std=np.array([ks[n][S.STD] for n in knames], np.float32))
+    from nvidia_resiliency_ext.straggler import _native
+    import ctypes
+    cc = _native.CaptureCounters()
+    _native.lib().nvrx_capture_stats(ctypes.byref(cc))
+    counters = {f: getattr(cc, f) for f, _ in _native.CaptureCounters._fields_}
     D.shutdown()
 
     t_rep = [r[0] for r in reports]
@@ -230,8 +236,9 @@ def main():
         strag = rep.identify_stragglers(gpu_rel_threshold=0.8, gpu_indiv_threshold=0.8)
         nrec = sum(int(v[straggler.Statistic.NUM]) for v in (local_ks or {}).values())
         line = {
-            "workload": "configs[4]: live rocprofiler-sdk dispatch capture, GPT-2 small DDP "
+            "workload": "configs[4]: live kernel-dispatch capture, GPT-2 small DDP "
                         f"(layers={a.layers}, batch={a.batch}x{a.seq}, bf16 autocast, AdamW)",
+            "capture_counters": counters,
             "n_gpus": ws, "capture": CAPTURE and cupti.capture_available(),
             "step_ms_without_detector": t_base * 1e3, "step_ms_with_detector": t_det * 1e3,
             "detector_overhead_pct": (t_det / t_base - 1) * 100,
