@@ -206,3 +206,27 @@ def test_two_in_flight_on_two_streams_keep_history_order(records, mode):
         np.testing.assert_array_equal(w.gpu_relative, g.gpu_relative)
         np.testing.assert_array_equal(w.gpu_individual, g.gpu_individual)
         np.testing.assert_array_equal(w.stragglers_individual, g.stragglers_individual)
+
+
+def test_launch_modes_agree_at_full_size():
+    """configs[1] at full size (64 x 2048 x 10,000 pushed, 8,192 kept): the bench's launch mode
+    (each report on its own stream, the stagger) and whole-report graphs on one stream give the same
+    scores, bit for bit, report for report (the individual history included), and the injected
+    straggler set."""
+    R, K, S = 64, 2048, 10000
+    ns = synth.synth_matrix(R, K, S, device="cuda")
+    res = {}
+    for mode in ("alt", "whole"):
+        rep = batch.MatrixReporter(R, K, cap=8192, thr_rel=0.8, thr_ind=0.8)
+        pipe = rep.pipelined(ns, S, mode=mode)
+        got = []
+        pipe.submit()
+        for i in range(6):
+            if i + 1 < 6:
+                pipe.submit()
+            got.append(pipe.collect()[0])
+        res[mode] = got
+    for a, b in zip(res["alt"], res["whole"]):
+        assert np.array_equal(a.gpu_relative.view(np.uint64), b.gpu_relative.view(np.uint64))
+        assert np.array_equal(a.gpu_individual.view(np.uint64), b.gpu_individual.view(np.uint64))
+        assert np.array_equal(a.stragglers_relative, synth.straggler_ranks(R).astype(bool))
