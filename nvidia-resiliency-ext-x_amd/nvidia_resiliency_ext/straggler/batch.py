@@ -465,7 +465,9 @@ class PipelinedReports:
     i-1's, so the individual history advances in submission order.  "side": every statistics
     phase on one stream, every rest on another (buffer sets per report in flight as in alt).
     "whole": one whole-report graph per report on the caller's stream (1 GPU).  "auto" (default):
-    alt for statistics phases up to PIPE_ALT_MAX_BYTES, else whole (side on N GPUs).  With two
+    alt for statistics phases up to PIPE_ALT_MAX_BYTES, else whole (side on N GPUs); on N GPUs
+    the choice takes the largest shard's bytes -- one all_reduce in the constructor, so every
+    rank constructs its PipelinedReports at the same point, as it calls report().  With two
     streams the inputs a report reads must not change until it is collected (collect() orders
     the caller's stream after it).  N GPUs (exchange): per report the statistics, the shard's
     partials and the combine (+ result copy) are graphs and the all_gather of the partials is
