@@ -121,8 +121,8 @@ hipError_t ragged_launch_classes(const RaggedSegs& segs, const uint32_t* cls_lis
     const uint32_t* list = cls_list;
     const int64_t need = aligned16 ? keep : keep + 3;
     // class kernels; classes that max_len rules out are not launched.  With side streams the
-    // classes are dealt round robin over them in launch order (fork / join by events, which HIP graph capture
-    // follows), so one class's tail and latency-bound waves overlap the next class.
+    // classes are dealt round robin over them in launch order (fork / join by events, which HIP
+    // graph capture follows), so one class's tail and latency-bound waves overlap the next class.
     std::lock_guard<std::mutex> lock(fork_mutex());
     Fork* fk = nullptr;
     if (hipError_t e = ragged_fork(st, fk); e != hipSuccess) return e;
