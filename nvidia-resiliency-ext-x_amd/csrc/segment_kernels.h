@@ -747,19 +747,14 @@ void seg_stats_lean_kernel(Segs segs, int64_t nseg, nvrx_stats_soa out, ColRef c
 #endif
 template <int PL, class Segs>
 __global__ __launch_bounds__(64 * NVRX_GROUP_WAVES) __attribute__((amdgpu_waves_per_eu(Occ<PL>::W)))
-void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, int64_t head, nvrx_stats_soa out,
-                                 ColRef cr) {
+void seg_stats_lean_group_kernel(Segs segs, int64_t nseg, int group, nvrx_stats_soa out, ColRef cr) {
     constexpr int NB = Bins<PL>::NB;
     __shared__ __attribute__((aligned(16))) unsigned lds_hist[NVRX_GROUP_WAVES * NB];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = lane_id();
-    // segments [0, head) in groups of `group` (head a multiple of it), the tail [head, nseg) one per
-    // wave: the last waves to start finish about together instead of a group apart
-    const int64_t wid = (int64_t)blockIdx.x * NVRX_GROUP_WAVES + wave;
-    const int64_t s0 = wid * group < head ? wid * group : head + (wid - head / group);
+    const int64_t s0 = ((int64_t)blockIdx.x * NVRX_GROUP_WAVES + wave) * group;
     if (s0 >= nseg) return;
-    const int64_t gcnt = s0 < head ? group : 1;
-    const int cnt = (int)(nseg - s0 < gcnt ? nseg - s0 : gcnt);
+    const int cnt = (int)(nseg - s0 < group ? nseg - s0 : group);
     unsigned* hist = lds_hist + wave * NB;
     unsigned a_mn = 0, a_mx = 0, a_k0 = 0, a_k1 = 0, a_c = 0, a_sdlo = 0, a_sdhi = 0, a_sqlo = 0, a_sqhi = 0;
     uint64_t wide = 0;
@@ -1166,21 +1161,6 @@ static_assert(NVRX_LEAN_GROUP_MAX >= 1 && NVRX_LEAN_GROUP_MAX <= 64, "NVRX_LEAN_
 #ifndef NVRX_LEAN_GROUP_WAVES  // build-time tuning constant: the fewest waves a grouped grid keeps
 #define NVRX_LEAN_GROUP_WAVES 32768
 #endif
-#ifndef NVRX_GROUP_TAIL  // build-time tuning constant: rounds of single-segment waves at the end
-#define NVRX_GROUP_TAIL 4
-#endif
-static inline int device_cus() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (cus[dev] == 0) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        cus[dev] = n;
-    }
-    return cus[dev];
-}
 static inline int lean_group(int64_t nseg) {
     const int64_t g = nseg / NVRX_LEAN_GROUP_WAVES;
     return g < 1 ? 1 : g > NVRX_LEAN_GROUP_MAX ? NVRX_LEAN_GROUP_MAX : (int)g;
@@ -1195,17 +1175,10 @@ static void launch_pl(const Segs& segs, int64_t nseg, bool full, const nvrx_stat
     if (full) {
         if constexpr (PL <= NVRX_LEAN_GROUP_PL_MAX) {
             const int g = lean_group(nseg);
-            // the tail taken one segment per wave: NVRX_GROUP_TAIL rounds of the resident waves
-            // (CUs x waves per SIMD x 4 SIMDs), when the grid is several rounds long
-            const int64_t resident = (int64_t)device_cus() * Occ<PL>::W * 4;
-            int64_t tail = g > 1 && nseg > 4 * resident * g ? (int64_t)NVRX_GROUP_TAIL * resident : 0;
-            int64_t head = nseg - tail;
-            head -= head % g;
-            tail = nseg - head;
-            const int64_t waves = head / g + tail;
+            const int64_t waves = (nseg + g - 1) / g;
             hipLaunchKernelGGL((seg_stats_lean_group_kernel<PL, Segs>),
                                dim3((unsigned)((waves + NVRX_GROUP_WAVES - 1) / NVRX_GROUP_WAVES)),
-                               dim3(64 * NVRX_GROUP_WAVES), 0, st, segs, nseg, g, head, out, cr);
+                               dim3(64 * NVRX_GROUP_WAVES), 0, st, segs, nseg, g, out, cr);
         } else {
             hipLaunchKernelGGL((seg_stats_lean_kernel<PL, Segs>), grid, block, 0, st, segs, nseg, out, cr);
         }

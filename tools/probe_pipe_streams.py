@@ -10,7 +10,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"))
+# AB_PKG: package root to import (a saved copy with another libnvrx_hip.so, tools/build_variant.sh)
+sys.path.insert(0, os.environ.get("AB_PKG", os.path.join(ROOT, "nvidia-resiliency-ext-x_amd")))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
