@@ -21,6 +21,8 @@ and the history are shard-local and the only exchange is the [R][6] f64 partials
 from __future__ import annotations
 
 import os
+import time
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -38,21 +40,60 @@ from . import ops
 FUSED_REF_MAX_ROWS = 256
 
 
-def _wait(device) -> None:
-    """Wait for the current stream by polling an event (the report's results land in pinned
-    host memory; a blocking synchronize adds the driver's wake-up latency to every report).
-    NVRX_SYNC=block restores the blocking wait."""
-    st = torch.cuda.current_stream(device)
-    if _SYNC_BLOCK:
-        st.synchronize()
+# How the host waits for a report's results (they land in pinned host memory):
+#   "bounded" (default) -- poll the completion event for at most SPIN_BOUND_US, then block in
+#       hipEventSynchronize on a blocking-sync event: a report that lands within the bound
+#       skips the driver's wake-up latency, a longer one does not hold a host core (in a
+#       training process that calls this API every core belongs to the job; the reference's
+#       report path blocks too, straggler.py:234-235, CuptiProfiler.cpp:136-146);
+#   "spin" -- poll until done (bench.py: the wake-up latency is part of every timed report);
+#   "block" -- block at once.
+# NVRX_SYNC selects the mode per process; set_sync_mode() changes it at run time.
+SYNC_MODES = ("bounded", "spin", "block")
+SPIN_BOUND_US = float(os.environ.get("NVRX_SPIN_US", "50"))
+_sync_mode = os.environ.get("NVRX_SYNC", "") or "bounded"
+if _sync_mode not in SYNC_MODES:
+    raise ValueError(f"NVRX_SYNC={_sync_mode!r}: one of {SYNC_MODES}")
+
+
+def set_sync_mode(mode: str) -> str:
+    """Select how report results are waited for (SYNC_MODES); returns the previous mode."""
+    global _sync_mode
+    if mode not in SYNC_MODES:
+        raise ValueError(f"sync mode {mode!r}: one of {SYNC_MODES}")
+    prev, _sync_mode = _sync_mode, mode
+    return prev
+
+
+def sync_mode() -> str:
+    return _sync_mode
+
+
+def wait_event(ev, mode: Optional[str] = None, bound_us: Optional[float] = None) -> None:
+    """Wait until a recorded event has completed, in the current (or the given) sync mode.
+    `ev` needs query() and synchronize(); the blocking fallback blocks only if the event was
+    created with blocking=True (every event this module waits on is)."""
+    mode = mode or _sync_mode
+    if mode == "block":
+        ev.synchronize()
         return
-    ev = torch.cuda.Event()
-    ev.record(st)
+    if mode == "spin":
+        while not ev.query():
+            pass
+        return
+    bound = SPIN_BOUND_US if bound_us is None else bound_us
+    deadline = time.perf_counter_ns() + int(bound * 1e3)
     while not ev.query():
-        pass
+        if time.perf_counter_ns() >= deadline:
+            ev.synchronize()
+            return
 
 
-_SYNC_BLOCK = os.environ.get("NVRX_SYNC", "") == "block"
+def _wait(device) -> None:
+    """Wait for the device's current stream (wait_event on an event recorded on it)."""
+    ev = torch.cuda.Event(blocking=True)
+    ev.record(torch.cuda.current_stream(device))
+    wait_event(ev)
 
 
 @dataclass
@@ -110,9 +151,26 @@ class MatrixReporter:
         # report is two launches (statistics, scores) with no initialising fill in between
         self.done = torch.zeros(2, dtype=torch.int32, device=d)
         self._colref_clean = False  # col_ref holds the initial reference (set by the epilogue)
+        self._pipes = weakref.WeakSet()  # PipelinedReports over this reporter
+
+    def _order_after_inflight(self, exclude=None) -> None:
+        """The caller's stream waits for every pipelined report still in flight on this reporter.
+        Those reports run on private streams and use slot 0's buffers (the reporter's own
+        statistics, reference and results) and the shared history, so an eager report, a graph
+        replay or a history reset issued between submit() and collect() queues behind them
+        instead of racing them.  A no-op while a graph is being captured (the captures pair
+        their phases themselves) and with nothing in flight."""
+        if not self._pipes or torch.cuda.is_current_stream_capturing():
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for p in list(self._pipes):
+            if p is not exclude:
+                for k, _ in p.pending:
+                    cur.wait_event(p.done[k])
 
     def reset_history(self):
         if self.hist is not None:
+            self._order_after_inflight()
             self.hist.fill_(float("inf"))
 
     # -- device phases, separately callable (bench times the stats kernel) --
@@ -128,6 +186,7 @@ class MatrixReporter:
     def compute_stats(self, ns: torch.Tensor, s_push: int) -> ops.SegmentStats:
         # (inside a graph capture the flag describes the device state when the graph replays:
         # the captured sequences always pair a statistics call with the scores that follow)
+        self._order_after_inflight()
         st = ops.segment_stats_strided(ns.view(-1), self.R * self.K, s_push, 0, s_push,
                                        cap=self.cap, mode=self.mode, out=self.stats,
                                        col_ref=self.col_ref if self._fuse_ref() else None,
@@ -139,6 +198,7 @@ class MatrixReporter:
     def compute_stats_records(self, recs: torch.Tensor, rec_off: torch.Tensor) -> ops.SegmentStats:
         """recs [n, 2] int32 {slot, ns} of R streams (rec_off [R+1] int64, device): the
         reference's ring pushes (CuptiProfiler.cpp:168-203) + getStats, for every rank."""
+        self._order_after_inflight()
         n = recs.shape[0]
         need = ops.records_bucket_capacity(n, self.R, self.K)
         b = getattr(self, "_bucket", None)
@@ -175,6 +235,7 @@ class MatrixReporter:
         RCCL all_gather -> finalize on N GPUs).  out_buf: another packed buffer of the same
         layout (1 GPU), e.g. pinned host memory the kernel writes directly (no copy)."""
         R, K = self.R, self.K
+        self._order_after_inflight()
         st = self.stats.view(R, K)
         ref = self.col_ref.view(torch.float32)[:K] if self.relative else None
         missing = self.col_ref[K:2 * K] if self.relative else None
@@ -254,20 +315,34 @@ class MatrixReporter:
         """graph() over record streams resident in HBM (compute_stats_records captured)."""
         return ReportGraph(self, None, 0, stats=lambda: self.compute_stats_records(recs, rec_off))
 
-    def pipelined(self, ns: torch.Tensor, s_push: int, timing: bool = False,
+    def pipelined(self, ns, s_push: int, timing: bool = False,
                   mode: Optional[str] = None, depth: int = 2) -> "PipelinedReports":
         """Reports replayed two deep: report i+1's device work is queued before report i's
         results are read on the host, each report landing in its own pinned buffer (N GPUs: the
-        partials exchange of each report stays an eager collective, issued in report order)."""
-        return PipelinedReports(self, ns, s_push, timing, mode=mode, depth=depth)
+        partials exchange of each report stays an eager collective, issued in report order).
+        ns: one input matrix, or a list of them (report i reads ns[i % len(ns)]; len(ns) divides
+        depth) -- e.g. a fresh matrix per report in flight.  An input must not be modified while
+        a report that reads it is in flight: collect() raises if a torch in-place operation
+        changed it (its version counter moved) between that report's submit() and collect()."""
+        ins = list(ns) if isinstance(ns, (list, tuple)) else [ns]
+        return PipelinedReports(self, None, s_push, timing, mode=mode, depth=depth,
+                                stats=[lambda x=x: self.compute_stats(x, s_push) for x in ins],
+                                stats_bytes=self._matrix_bytes(s_push), inputs=[(x,) for x in ins])
 
-    def pipelined_records(self, recs: torch.Tensor, rec_off: torch.Tensor,
+    def _matrix_bytes(self, s_push: int) -> int:
+        keep = min(s_push, self.cap) if self.cap > 0 else s_push
+        return 4 * self.R * self.K * keep  # 4 B per retained sample
+
+    def pipelined_records(self, recs, rec_off: torch.Tensor,
                           timing: bool = False, mode: Optional[str] = None) -> "PipelinedReports":
         """pipelined() over record streams resident in HBM (compute_stats_records: bucketing,
         classification and the class kernels -- side-stream fork / join and stream-ordered
-        scratch included -- captured into the report graphs)."""
-        return PipelinedReports(self, None, 0, timing, mode=mode, stats_bytes=8 * recs.shape[0],
-                                stats=lambda: self.compute_stats_records(recs, rec_off))
+        scratch included -- captured into the report graphs).  recs: one record tensor or a list
+        of them (same layout, rec_off shared), as ns for pipelined()."""
+        ins = list(recs) if isinstance(recs, (list, tuple)) else [recs]
+        return PipelinedReports(self, None, 0, timing, mode=mode, stats_bytes=8 * ins[0].shape[0],
+                                stats=[lambda r=r: self.compute_stats_records(r, rec_off) for r in ins],
+                                inputs=[(r, rec_off) for r in ins])
 
     def _unpack(self, buf: Optional[torch.Tensor] = None) -> BatchResult:
         R = self.R
@@ -330,11 +405,13 @@ class ReportGraph:
 
     def run_stats(self) -> None:
         self._check_clean()
+        self.rep._order_after_inflight()
         self.stats.replay()
         self.rep._colref_clean = False
 
     def run_rest(self) -> BatchResult:
         rep = self.rep
+        rep._order_after_inflight()
         if self.rest is None:  # N GPUs: partials graph, eager all_gather, combine graph
             self.partials.replay()
             rep._colref_clean = rep._fuse_ref()
@@ -352,6 +429,7 @@ class ReportGraph:
             self.run_stats()
             return self.run_rest()
         self._check_clean()
+        self.rep._order_after_inflight()
         self.full.replay()
         self.rep._colref_clean = self.rep._fuse_ref()
         _wait(self.rep.device)
@@ -364,6 +442,7 @@ def _warm_up(rep: MatrixReporter, stats) -> None:
     warm-up must not fold whatever the inputs hold now into it (the graphs' reports advance it
     exactly as report() does)."""
     d = rep.device
+    rep._order_after_inflight()
     saved = rep.hist.clone() if rep.hist is not None else None
     side = torch.cuda.Stream(d)
     side.wait_stream(torch.cuda.current_stream(d))
@@ -477,16 +556,30 @@ class PipelinedReports:
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
     statistics kernel on an otherwise idle device, for a sample of the reports.
-    stats: the statistics phase as a callable (default: compute_stats(ns, s_push); record
-    streams: MatrixReporter.pipelined_records)."""
+    stats: the statistics phase as a callable, or a list of them, one per input set (report i
+    runs stats[i % len(stats)]; default: compute_stats(ns, s_push); record streams:
+    MatrixReporter.pipelined_records).  inputs: per input set, the tensors its statistics phase
+    reads; collect() raises if one of them was modified in place by torch while the report was
+    in flight.
+    Other work on the same reporter (report(), a ReportGraph, compute_stats, reset_history)
+    issued before collect() is ordered after the reports in flight
+    (MatrixReporter._order_after_inflight)."""
 
     def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int,
                  timing: bool = False, stats=None, mode: Optional[str] = None,
-                 stats_bytes: Optional[int] = None, depth: int = 2):
+                 stats_bytes: Optional[int] = None, depth: int = 2, inputs=None):
         self.mode = mode or _PIPE_MODE or "auto"
         if stats_bytes is None:  # the matrix path: 4 B per retained sample
-            keep = min(s_push, rep.cap) if rep.cap > 0 else s_push
-            stats_bytes = 4 * rep.R * rep.K * keep
+            stats_bytes = rep._matrix_bytes(s_push)
+        if stats is None:
+            stats = [lambda: rep.compute_stats(ns, s_push)]  # noqa: E731
+            inputs = [(ns,)] if inputs is None else inputs
+        elif callable(stats):
+            stats = [stats]
+        self.inputs = list(inputs) if inputs is not None else [() for _ in stats]
+        if len(self.inputs) != len(stats) or depth % len(stats) != 0:
+            raise ValueError(f"pipelined reports: {len(stats)} input sets for depth {depth} "
+                             "(one inputs entry per set; the set count divides depth)")
         if self.mode == "auto":
             if rep.exchange and rep.world > 1:  # one mode on every rank (shards differ in size)
                 x = torch.tensor([float(stats_bytes)], dtype=torch.float64,
@@ -504,8 +597,6 @@ class PipelinedReports:
             raise ValueError("pipelined reports: depth >= 2 (> 2 with two streams only)")
         self.depth = depth
         self.rep, self.timing = rep, timing
-        if stats is None:
-            stats = lambda: rep.compute_stats(ns, s_push)  # noqa: E731
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(depth)]
 
         def scores(k: int):
@@ -522,7 +613,7 @@ class PipelinedReports:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 if with_stats:
-                    stats()
+                    stats[k % len(stats)]()
                 if rest:
                     scores(k)
             return g
@@ -538,7 +629,7 @@ class PipelinedReports:
             self.stats_g, self.rest_g, self.part_g, self.fin_g = [], [], [], []
             for k, slot in enumerate(self.slots):
                 with slot.bind(rep):
-                    _warm_up(rep, stats)  # initialises this slot's column reference too
+                    _warm_up(rep, stats[k % len(stats)])  # initialises this slot's column reference too
                     self.stats_g.append(capture(True, False, k))
                     if rep.exchange:  # N GPUs: partials | eager all_gather | combine + result copy
                         self.part_g.append(capture_fn(rep._scores_partials))
@@ -551,7 +642,7 @@ class PipelinedReports:
             self.hist_done = [torch.cuda.Event() for _ in range(depth)]
             self.stats_done = [torch.cuda.Event() for _ in range(depth)]
         else:
-            _warm_up(rep, stats)
+            _warm_up(rep, stats[0])
             self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
             self.full = [capture(True, True, k) for k in range(2)]
             if timing:
@@ -559,7 +650,9 @@ class PipelinedReports:
                 self.rest = [capture(False, True, k) for k in range(2)]
         if timing:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        self.done = [torch.cuda.Event() for _ in range(depth)]
+        # blocking-sync events: wait_event's fallback sleeps instead of polling
+        self.done = [torch.cuda.Event(blocking=True) for _ in range(depth)]
+        self._versions = [None] * depth  # the inputs' version counters at each slot's submit
         # the one-time stagger of a burst's second report: a quarter of the statistics phase at
         # ~6.5 TB/s (STAGGER_FRAC; NVRX_PIPE_STAGGER=0 disables), in spin cycles of ~2.2 GHz
         frac = float(os.environ.get("NVRX_PIPE_STAGGER", STAGGER_FRAC))
@@ -568,6 +661,7 @@ class PipelinedReports:
         self.pending = []  # (slot, timed) in flight, oldest first
         self.ready = []    # results collected early (a timed submit drains), oldest first
         self.n = 0
+        rep._pipes.add(self)
 
     def submit(self, timed: bool = False) -> None:
         """Queue the next report (at most `depth` in flight: collect() the oldest first)."""
@@ -582,12 +676,13 @@ class PipelinedReports:
         if timed:
             while self.pending:  # the device idles before the measured statistics phase
                 self.ready.append(self._land())
+        self.rep._order_after_inflight(exclude=self)  # another pipeline's reports on this reporter
+        self._versions[k] = [t._version for t in self.inputs[k % len(self.inputs)]]
+        if timed:
             # a short spin keeps the device busy while the host queues the graphs, so the
             # first event fires right before the statistics phase rather than a graph-launch
             # latency ahead of it
-            spin = getattr(torch.cuda, "_sleep", None)  # torch's spin kernel (private API)
-            if spin is not None:
-                spin(TIMED_SPIN_CYCLES)
+            _spin(TIMED_SPIN_CYCLES)
         if self.alt:
             # alt: report i on stream i % 2; side: every statistics phase on stream 0, every rest
             # on stream 1 (slot k's previous report has finished with its buffers: done[k])
@@ -650,13 +745,14 @@ class PipelinedReports:
     def _land(self):
         k, timed = self.pending.pop(0)
         ev = self.done[k]
-        if _SYNC_BLOCK:
-            ev.synchronize()
-        else:
-            while not ev.query():
-                pass
+        wait_event(ev)
         if self.alt:  # the caller's later work (new inputs, the history) follows this report
             torch.cuda.current_stream(self.rep.device).wait_event(ev)
+        now = [t._version for t in self.inputs[k % len(self.inputs)]]
+        if now != self._versions[k]:
+            raise RuntimeError("PipelinedReports: an input of this report was modified in place "
+                               "while the report was in flight (submit() -> collect()); its "
+                               "results are undefined -- modify inputs only after collect()")
         ms = self.ev[0].elapsed_time(self.ev[1]) if timed else None
         return self.rep._unpack(self.bufs[k]), ms
 

@@ -230,3 +230,96 @@ def test_launch_modes_agree_at_full_size():
         assert np.array_equal(a.gpu_relative.view(np.uint64), b.gpu_relative.view(np.uint64))
         assert np.array_equal(a.gpu_individual.view(np.uint64), b.gpu_individual.view(np.uint64))
         assert np.array_equal(a.stragglers_relative, synth.straggler_ranks(R).astype(bool))
+
+
+def _same(w, g):
+    for f in ("gpu_relative", "gpu_individual"):
+        assert np.array_equal(getattr(w, f).view(np.uint64), getattr(g, f).view(np.uint64)), f
+    np.testing.assert_array_equal(w.stragglers_relative, g.stragglers_relative)
+    np.testing.assert_array_equal(w.stragglers_individual, g.stragglers_individual)
+
+
+@pytest.mark.parametrize("records", [False, True])
+def test_eager_work_while_reports_in_flight_is_ordered(records):
+    """in the two-stream modes slot 0 is the reporter's own buffer set and
+    the history is shared, so report(), a history reset or a graph replay issued between
+    submit() and collect() must queue behind the reports in flight.  The mixed sequence gives,
+    bit for bit, what the same calls give one at a time on a fresh reporter."""
+    R, K = 64, 512
+    if records:
+        counts = synth.zipf_counts(K, top=2000)
+        slot, occ = synth.zipf_order(counts)
+        t = lambda a: torch.from_numpy(a.view(np.int32)).cuda()  # noqa: E731
+        src = [synth.synth_records(R, t(slot), t(occ), K, int(counts.max()), seed=60 + i) for i in range(2)]
+        off = torch.arange(R + 1, dtype=torch.int64, device="cuda") * slot.size
+        mk = lambda: batch.MatrixReporter(R, K, cap=1024, thr_rel=0.8, thr_ind=0.8)  # noqa: E731
+        a, b = mk(), mk()
+        run = lambda rep, x: rep.report_records(x, off)  # noqa: E731
+        pipe = b.pipelined_records(src[0], off, mode="alt")
+        g = b.graph_records(src[1], off)
+    else:
+        S = 3000
+        src = [synth.synth_matrix(R, K, S, seed=60 + i, device="cuda") for i in range(2)]
+        mk = lambda: batch.MatrixReporter(R, K, cap=2048, thr_rel=0.8, thr_ind=0.8)  # noqa: E731
+        a, b = mk(), mk()
+        run = lambda rep, x: rep.report(x, S)  # noqa: E731
+        pipe = b.pipelined(src[0], S, mode="alt")
+        g = b.graph(src[1], S)
+    want = [run(a, src[0]), run(a, src[1]), run(a, src[0]), run(a, src[0])]
+    a.reset_history()
+    want += [run(a, src[1]), run(a, src[0]), run(a, src[1])]
+    got = []
+    pipe.submit()                     # report 1 (src0) in flight on a private stream
+    e1 = run(b, src[1])               # report 2, eager, on the caller's stream
+    got += [pipe.collect()[0], e1]
+    pipe.submit()                     # reports 3, 4 in flight
+    pipe.submit()
+    b.reset_history()                 # after both
+    e5 = g.run()                      # report 5 (src1) as a graph replay
+    got += [pipe.collect()[0], pipe.collect()[0], e5]
+    pipe.submit()                     # report 6 in flight, then report 7 eager
+    e7 = run(b, src[1])
+    got += [pipe.collect()[0], e7]
+    assert len(got) == len(want)
+    for w, x in zip(want, got):
+        _same(w, x)
+
+
+@pytest.mark.parametrize("mode", ["alt", "whole"])
+def test_distinct_inputs_per_report_in_flight(mode):
+    """pipelined([x0, x1]): report i reads x[i % 2] (bench.py's input-independence control for
+    the headline) -- report for report the eager reports over the alternating inputs."""
+    R, K, S = 32, 256, 1500
+    src = [synth.synth_matrix(R, K, S, seed=80 + i, device="cuda") for i in range(2)]
+    a = batch.MatrixReporter(R, K, cap=1024, thr_rel=0.8, thr_ind=0.8)
+    b = batch.MatrixReporter(R, K, cap=1024, thr_rel=0.8, thr_ind=0.8)
+    want = [a.report(src[i % 2], S) for i in range(6)]
+    pipe = b.pipelined(src, S, mode=mode, timing=True)
+    got = []
+    pipe.submit()
+    for i in range(6):
+        if i + 1 < 6:
+            pipe.submit()
+        got.append(pipe.collect()[0])
+    for w, x in zip(want, got):
+        _same(w, x)
+    with pytest.raises(ValueError):  # three input sets do not divide depth 2
+        b.pipelined(src + [src[0]], S, mode=mode)
+
+
+def test_input_modified_in_flight_is_refused():
+    """An input changed by a torch in-place op between submit() and collect() is reported
+    (the version counter of the tensor moved); changes between reports are fine."""
+    R, K, S = 8, 64, 500
+    ns = synth.synth_matrix(R, K, S, device="cuda")
+    rep = batch.MatrixReporter(R, K, cap=256, thr_rel=0.8, thr_ind=0.8)
+    pipe = rep.pipelined(ns, S)
+    pipe.submit()
+    pipe.collect()
+    ns.add_(0)        # between reports: allowed
+    pipe.submit()
+    ns.add_(0)        # while the report reads it
+    with pytest.raises(RuntimeError, match="modified in place"):
+        pipe.collect()
+    pipe.submit()
+    pipe.collect()    # the pipeline goes on

@@ -102,3 +102,57 @@ def test_detection_section_fails_if_not_initialized():
     with pytest.raises(RuntimeError):
         with straggler.Detector.detection_section("section00"):
             pass
+
+
+class _FakeEvent:
+    """query() turns True after `ready_after` polls (never when None); synchronize() is
+    recorded with the time it was called."""
+
+    def __init__(self, ready_after=None):
+        import time
+        self.t0 = time.perf_counter_ns()
+        self.ready_after, self.polls, self.sync_at = ready_after, 0, None
+
+    def query(self):
+        self.polls += 1
+        return self.ready_after is not None and self.polls > self.ready_after
+
+    def synchronize(self):
+        import time
+        self.sync_at = time.perf_counter_ns() - self.t0
+
+
+def test_wait_event_bounded_spin_then_block():
+    """the default wait polls for at most SPIN_BOUND_US, then blocks in
+    synchronize() (a blocking-sync event) instead of holding a host core for the whole report."""
+    from nvidia_resiliency_ext.straggler import batch
+
+    assert batch.sync_mode() == "bounded" or "NVRX_SYNC" in __import__("os").environ
+    never = _FakeEvent(ready_after=None)  # a long report: the bound expires, then block
+    batch.wait_event(never, mode="bounded", bound_us=50)
+    assert never.sync_at is not None and never.polls >= 1
+    # the poll loop stopped at the bound (50 us), not after the whole wait; generous slack for
+    # a loaded CI host
+    assert never.sync_at < 50_000_000, never.sync_at
+    quick = _FakeEvent(ready_after=3)  # lands within the bound: no blocking call at all
+    batch.wait_event(quick, mode="bounded", bound_us=1e6)
+    assert quick.sync_at is None and quick.polls == 4
+    spin = _FakeEvent(ready_after=200)  # "spin" (bench.py) never blocks
+    batch.wait_event(spin, mode="spin")
+    assert spin.sync_at is None and spin.polls == 201
+    block = _FakeEvent(ready_after=None)  # "block" blocks at once, no polling
+    batch.wait_event(block, mode="block")
+    assert block.sync_at is not None and block.polls == 0
+
+
+def test_sync_mode_switch():
+    from nvidia_resiliency_ext.straggler import batch
+
+    prev = batch.set_sync_mode("spin")
+    try:
+        assert batch.sync_mode() == "spin"
+        with pytest.raises(ValueError):
+            batch.set_sync_mode("busy")
+    finally:
+        batch.set_sync_mode(prev)
+    assert batch.sync_mode() == prev
