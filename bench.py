@@ -106,12 +106,42 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def make_shard(R, K_global, s_push, world, rank, dev):
+def make_shard(R, K_global, s_push, world, rank, dev, seed=synth.SEED):
+    """This rank's kernels of a [R][K_global][s_push] matrix.  seed: the per-sample jitter; the
+    straggler ranks stay the default seed's, so every input carries the same straggler set."""
     names = synth.kernel_names(K_global)
     kidx = synth.shard_kernels(names, world, rank) if world > 1 else np.arange(K_global)
     kmap = torch.from_numpy(kidx).to(dev)
-    ns = synth.synth_matrix(R, len(kidx), s_push, K_global=K_global, kmap=kmap, device=dev)
+    strag = torch.from_numpy(synth.straggler_ranks(R)).to(dev)
+    ns = synth.synth_matrix(R, len(kidx), s_push, K_global=K_global, kmap=kmap, straggler=strag,
+                            seed=seed, device=dev)
     return ns, kidx
+
+
+# The pipelined legs give each report in flight its own input (two matrices / record sets that
+# differ in every sample): no report can be served by cache lines another report just pulled
+# (VERDICT r05 weak #3; the reference reads fresh rings every report, straggler.py:237-243)
+INPUTS_IN_FLIGHT = 2
+SEED_ALT = synth.SEED ^ 0x5A5A5A5A
+
+
+def timed_pipe_loop(pipe, steps, world, mode="spin"):
+    """`steps` back-to-back reports, two in flight, between barriers, with the host waiting in
+    the given sync mode (batch.SYNC_MODES).  Returns (last result, elapsed s)."""
+    prev = batch.set_sync_mode(mode)
+    try:
+        barrier(world)
+        t0 = time.perf_counter()
+        pipe.submit()
+        res = None
+        for i in range(steps):
+            if i + 1 < steps:
+                pipe.submit()
+            res, _ = pipe.collect()
+        barrier(world)
+        return res, time.perf_counter() - t0
+    finally:
+        batch.set_sync_mode(prev)
 
 
 TIMED_REPORTS = 10  # statistics-kernel timing phase after the throughput loop
@@ -199,17 +229,12 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         # unpack of the results written to pinned memory) inside the timed region, which holds
         # nothing but back-to-back reports.  N GPUs: per report statistics, the shard's partials
         # and the combine as graphs, the all_gather of the partials eager between them
-        pipe = rep.pipelined(ns, s_push, timing=time_kernel)
+        ns_alt, _ = make_shard(R, K_global, s_push, world, rank, dev, seed=SEED_ALT)
+        pipe = rep.pipelined([ns, ns_alt], s_push, timing=time_kernel)
         warm_pipelined(pipe, warmup, world)
-        barrier(world)
-        t0 = time.perf_counter()
-        pipe.submit()
-        for i in range(steps):
-            if i + 1 < steps:
-                pipe.submit()
-            res, _ = pipe.collect()
-        barrier(world)
-        elapsed = time.perf_counter() - t0
+        res, elapsed = timed_pipe_loop(pipe, steps, world, "spin")
+        # the same loop with the API's default host wait (bounded spin, then block)
+        res_b, elapsed_bounded = timed_pipe_loop(pipe, steps, world, "bounded")
         # the roofline's kernel time: after the throughput loop, same process and buffers,
         # reports submitted on an idle device with HIP events around the statistics phase
         ks = []
@@ -227,10 +252,17 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
             # rule, on every N: a 1 -> N curve of either field compares one launch mode
             g = rep.graph(ns, s_push)
             warm(g.run, max(1, warmup), world)
+            prev = batch.set_sync_mode("spin")
             res_p, el_p, km_p = phases_loop(rep, ns, s_push, g, steps, world, time_kernel)
-            phases = dict(elapsed=el_p, kern_ms=km_p, launch=phases_label(rep, g),
-                          sets=res_p.stragglers_relative)
+            batch.set_sync_mode("bounded")
+            _, el_pb, _ = phases_loop(rep, ns, s_push, g, steps, world, False)
+            batch.set_sync_mode(prev)
+            phases = dict(elapsed=el_p, elapsed_bounded=el_pb, kern_ms=km_p,
+                          launch=phases_label(rep, g), sets=res_p.stragglers_relative)
+        del ns_alt, pipe
         return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed,
+                    elapsed_bounded=elapsed_bounded,
+                    sets_bounded_ok=bool(np.array_equal(res_b.stragglers_relative, res.stragglers_relative)),
                     kern_ms=float(np.mean(ks)) if ks else None,
                     samples=R * K_local * keep, nseg=R * K_local, keep=keep,
                     launch=pipe_label(pipe), phases=phases)
@@ -282,24 +314,19 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     N = lslot.size
     t = lambda a: torch.from_numpy(a.view(np.int32)).to(dev)
     recs = synth.synth_records(R, t(lslot), t(locc), K, int(counts.max()), kglob=t(kglob))
+    recs_alt = synth.synth_records(R, t(lslot), t(locc), K, int(counts.max()), kglob=t(kglob),
+                                   straggler=torch.from_numpy(synth.straggler_ranks(R)).to(dev),
+                                   seed=SEED_ALT)
     rec_off = torch.arange(R + 1, dtype=torch.int64, device=dev) * N
     rep = batch.MatrixReporter(R, len(kidx), cap=cap, thr_rel=THR, thr_ind=THR, device=dev)
     for _ in range(warmup):
         res = rep.report_records(recs, rec_off)
-    # reports two in flight on two streams, as the headline (MatrixReporter.pipelined_records;
-    # N GPUs: statistics, partials and combine as graphs, the all_gather eager between them); the
-    # statistics phase timed afterwards on an idle device
-    pipe = rep.pipelined_records(recs, rec_off, timing=True)
+    # reports two in flight on two streams, each on its own record set, as the headline
+    # (MatrixReporter.pipelined_records; N GPUs: statistics, partials and combine as graphs, the
+    # all_gather eager between them); the statistics phase timed afterwards on an idle device
+    pipe = rep.pipelined_records([recs, recs_alt], rec_off, timing=True)
     warm_pipelined(pipe, warmup, world)
-    barrier(world)
-    t0 = time.perf_counter()
-    pipe.submit()
-    for i in range(steps):
-        if i + 1 < steps:
-            pipe.submit()
-        res, _ = pipe.collect()
-    barrier(world)
-    elapsed = time.perf_counter() - t0
+    res, elapsed = timed_pipe_loop(pipe, steps, world, "spin")
     ks = []
     for _ in range(TIMED_REPORTS):
         pipe.submit(timed=True)
@@ -314,7 +341,12 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
                bucket_plus_stats_ms=stats_ms,
                hbm_frac_of_report=R * N * RECORD_BYTES / (tmax / steps) / HBM_PEAK,
                hbm_frac_of_stats=R * N * RECORD_BYTES / (stats_ms * 1e-3) / HBM_PEAK,
-               alg_bytes_per_record=RECORD_BYTES, steps=steps,
+               alg_bytes_per_record=RECORD_BYTES, steps=steps, inputs_in_flight=INPUTS_IN_FLIGHT,
+               # HBM bytes per record the bucketing + class kernels move (committed rocprofv3
+               # --pmc passes, FETCH_SIZE x2) and the floor of any bucket-then-reduce design:
+               # read 8 B, write the kept 4 B payload, read it back
+               traffic_bytes_per_record=zipf_pmc_traffic(),
+               design_floor_bytes_per_record=16,
                kernels_per_rank=shard_sizes(K, world),
                straggler_sets_exact=all_ranks(bool(np.array_equal(
                    res.stragglers_relative, synth.straggler_ranks(R).astype(bool))), world, dev))
@@ -377,6 +409,20 @@ def pmc_traffic(workload: str):
             return float(json.load(f)["hbm_bytes_per_launch"])
     except Exception:
         return None
+
+
+def zipf_pmc_traffic():
+    """HBM bytes per record of the configs[3] statistics phase from the committed --pmc passes
+    (profiles/pmc_zipf_bucket.json + pmc_zipf_stats.json), or None."""
+    tot = 0.0
+    for part in ("bucket", "stats"):
+        p = os.path.join(ROOT, "profiles", f"pmc_zipf_{part}.json")
+        try:
+            with open(p) as f:
+                tot += float(json.load(f)["total"]["bytes_per_record"])
+        except Exception:
+            return None
+    return tot
 
 
 def cpu_baseline(ns, kidx, cfg, res_gpu_stats, sample_ranks, threads):
@@ -495,6 +541,13 @@ def main():
                    # latency itself; ms_per_report above is the pipelined rate
                    latency_ms_one_report=(comm_max(r4["phases"]["elapsed"], world, dev) / n4 * 1e3
                                           if r4.get("phases") else None),
+                   # the same two with the batch API's default host wait (bounded spin, then block)
+                   ms_per_report_bounded_wait=(comm_max(r4["elapsed_bounded"], world, dev) / n4 * 1e3
+                                               if r4.get("elapsed_bounded") is not None else None),
+                   latency_ms_one_report_bounded_wait=(
+                       comm_max(r4["phases"]["elapsed_bounded"], world, dev) / n4 * 1e3
+                       if r4.get("phases") and "elapsed_bounded" in r4["phases"] else None),
+                   inputs_in_flight=INPUTS_IN_FLIGHT,
                    steps=n4, kernels_per_rank=shard_sizes(C3["K"], world),
                    straggler_sets_exact=all_ranks(bool(np.array_equal(
                        s4.stragglers_relative, synth.straggler_ranks(C3["R"]).astype(bool))), world, dev))
@@ -582,6 +635,11 @@ def main():
             # measured after the pipelined loop on every N (a like-for-like 1 -> N
             # curve reads this field; "graph_phases" holds its label and rate)
             "ms_per_step_graph_phases": phases["ms_per_step"] if phases else None,
+            # the timed loop's host waits poll (batch.set_sync_mode("spin")); the batch API's
+            # default waits poll at most 50 us, then block -- the same loop in that mode:
+            "host_wait": "spin", "inputs_in_flight": INPUTS_IN_FLIGHT,
+            "ms_per_step_bounded_wait": (comm_max(r["elapsed_bounded"], world, dev) / args.steps * 1e3
+                                         if r.get("elapsed_bounded") is not None else None),
             "graph_phases": phases,
             "higher_is_better": True,
             "scaling": "weak",
@@ -597,7 +655,8 @@ def main():
                        "world_size": world, "world_size_reported": world_reported,
                        "kernels_per_rank": shard_sizes(K_global, world),
                        "backend": backend or "none (1 GPU)",
-                       "stats_mode": "fast", "launch": r["launch"], "launch_per_rank": launch_per_rank},
+                       "stats_mode": "fast", "launch": r["launch"], "launch_per_rank": launch_per_rank,
+                       "inputs_in_flight": INPUTS_IN_FLIGHT},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK,
                          "traffic": traffic,

@@ -1,7 +1,9 @@
-"""GPU: configs[4] live capture end to end -- a (reduced) GPT-2 DDP loop under the Detector
-(tools/live_gpt2.py, RCCL world of 1), kernel dispatches captured by rocprofiler-sdk into
-the device record log; the report's per-kernel statistics are checked bit for bit against
-the oracle's ring-push + computeStats restatement over the very records captured."""
+"""GPU: configs[4] live capture end to end -- the GPT-2 small DDP loop (12 layers, d=768, ctx
+1024; tools/live_gpt2.py, RCCL world of 1) under the Detector, kernel dispatches captured into
+the device record log; the report's per-kernel statistics are checked bit for bit against the
+oracle's ring-push + computeStats restatement over the very records captured, and every report
+window holds exactly its steps' launches.  The 2-rank DDP run of the same model with a slowed
+rank is tests/test_gpu_functional_ddp.py::test_gpt2_ddp_slow_rank_is_detected."""
 import json
 import os
 import random
@@ -22,14 +24,17 @@ def test_live_gpt2_capture_stats_match_oracle(tmp_path):
     out = tmp_path / "live.json"
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(random.randint(20000, 40000)),
                RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
-    cmd = [sys.executable, os.path.join(ROOT, "tools", "live_gpt2.py"), "--layers", "2",
-           "--batch", "2", "--seq", "256", "--warmup", "2", "--base-steps", "3", "--steps", "10",
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "live_gpt2.py"), "--layers", "12",
+           "--batch", "4", "--seq", "1024", "--warmup", "2", "--base-steps", "5", "--steps", "10",
            "--report-every", "5", "--count-check", "--dump", str(dump), "--out", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads(out.read_text())
+    print({k: res[k] for k in ("workload", "step_ms_without_detector", "step_ms_with_detector",
+                               "detector_overhead_pct", "report_ms_median", "records_per_report",
+                               "kernel_keys")})
     assert res["capture"] is True
-    assert res["kernel_keys"] > 20 and res["records_per_report"] > 100
+    assert res["kernel_keys"] > 50 and res["records_per_report"] > 1000
     assert res["gpu_relative_perf_scores"] == {"0": 1.0} or res["gpu_relative_perf_scores"] == {0: 1.0}
     # completeness (no explicit flush before the reports): every 5-step window holds exactly
     # 5 x each key's launches of a one-step window -- nothing lost, nothing carried over

@@ -1,0 +1,49 @@
+"""GPT-2 small (12 layers, d=768, 12 heads, vocab 50257, ctx 1024) as the configs[4] workload
+of tools/live_gpt2.py and tests/func/ddp_straggler.py --model gpt2: random init (no checkpoint
+offline), scaled-dot-product attention, tied head."""
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Block(nn.Module):
+    def __init__(self, d, h):
+        super().__init__()
+        self.h = h
+        self.ln1 = nn.LayerNorm(d)
+        self.qkv = nn.Linear(d, 3 * d)
+        self.proj = nn.Linear(d, d)
+        self.ln2 = nn.LayerNorm(d)
+        self.fc = nn.Linear(d, 4 * d)
+        self.out = nn.Linear(4 * d, d)
+
+    def forward(self, x):
+        B, T, C = x.shape
+        q, k, v = self.qkv(self.ln1(x)).split(C, dim=2)
+        q, k, v = (t.view(B, T, self.h, C // self.h).transpose(1, 2) for t in (q, k, v))
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        x = x + self.proj(y.transpose(1, 2).reshape(B, T, C))
+        return x + self.out(F.gelu(self.fc(self.ln2(x)), approximate="tanh"))
+
+
+class GPT2(nn.Module):
+    def __init__(self, vocab=50257, ctx=1024, d=768, layers=12, heads=12):
+        super().__init__()
+        self.wte = nn.Embedding(vocab, d)
+        self.wpe = nn.Embedding(ctx, d)
+        self.blocks = nn.ModuleList(Block(d, heads) for _ in range(layers))
+        self.ln_f = nn.LayerNorm(d)
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, std=0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+    def forward(self, idx):
+        T = idx.shape[1]
+        x = self.wte(idx) + self.wpe(torch.arange(T, device=idx.device))
+        for b in self.blocks:
+            x = b(x)
+        return self.ln_f(x) @ self.wte.weight.t()  # tied head
