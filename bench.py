@@ -259,13 +259,14 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
             batch.set_sync_mode(prev)
             phases = dict(elapsed=el_p, elapsed_bounded=el_pb, kern_ms=km_p,
                           launch=phases_label(rep, g), sets=res_p.stragglers_relative)
+        label = pipe_label(pipe)
         del ns_alt, pipe
         return dict(ns=ns, kidx=kidx, rep=rep, res=res, elapsed=elapsed,
                     elapsed_bounded=elapsed_bounded,
                     sets_bounded_ok=bool(np.array_equal(res_b.stragglers_relative, res.stragglers_relative)),
                     kern_ms=float(np.mean(ks)) if ks else None,
                     samples=R * K_local * keep, nseg=R * K_local, keep=keep,
-                    launch=pipe_label(pipe), phases=phases)
+                    launch=label, phases=phases)
     # eager launches (--no-graph), one report at a time
     res, elapsed, kern_ms = phases_loop(rep, ns, s_push, None, steps, world, time_kernel)
     keep = min(s_push, cap)

@@ -10,10 +10,11 @@ hundreds of distinct kernel keys (GEMMs, attention, layer norms, the fused optim
 Slowness is injected, as the test environment has one GPU for all ranks: every forward ends
 with a spin kernel (torch.cuda._sleep: same launch shape on every rank, so the same composite
 kernel key) that runs --slow-factor times longer on the ranks in --slow-ranks.  --spin-ratio r
-sizes the fast ranks' spin to r x the forward's measured GPU time (the largest over ranks), so
+sizes the fast ranks' spin to r x the forward's kernel time per step as the detector weighs it
+(sum of NUM x AVG over the captured forward kernels, the largest over ranks), so
 that the spin carries a known share of the NUM*AVG weights whatever the model: with forward
 time F and spin rF, a rank slowed s-fold scores (F + rF) / (F + s rF) (reporting.py:219-253),
-0.714 at r = 4, s = 1.5.  Launched with torch.distributed.run; gloo process group, all ranks on
+0.7 at r = 6, s = 1.5.  Launched with torch.distributed.run; gloo process group, all ranks on
 GPU LOCAL_RANK % device_count.  Prints the step time without and with the detector."""
 import argparse
 import os
@@ -111,6 +112,9 @@ def print_stragglers(st):
 
 def main():
     args = parse_args()
+    if os.environ.get("NVRX_FUNC_WATCHDOG_S"):  # diagnostics: every thread's stack, then exit
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["NVRX_FUNC_WATCHDOG_S"]), exit=True)
     torch.distributed.init_process_group("gloo")
     rank = torch.distributed.get_rank()
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
@@ -154,9 +158,13 @@ def main():
                 return model(x)
         return model(x)
 
-    def step():
+    def step(prof=None):
         x, tgt = batch_fn()
+        if prof is not None:
+            prof.start()
         out = fwd(x)
+        if prof is not None:
+            prof.stop()
         opt.zero_grad()
         if args.model == "gpt2":
             with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -167,20 +175,42 @@ def main():
         opt.step()
 
     base = args.spin_cycles
+    for _ in range(2):
+        step()
     if args.spin_ratio > 0:
-        # the forward's GPU time (no spin yet) and the spin's clock rate, both measured here;
-        # the largest forward time over ranks sets one base spin for every rank
-        with torch.no_grad():
-            f_ms = gpu_ms(lambda: fwd(batch_fn()[0]))
+        # the forward's kernel time per step as the detector weighs it -- sum of NUM x MED of the
+        # forward's captured kernels (reporting.py:248 weighs NUM x AVG) over 5 training steps, on a profiler
+        # handle of its own (closed before the Detector creates its singleton); the ranks share
+        # one GPU, so their kernels' durations include the other rank's concurrent work.  The
+        # largest over ranks sizes one base spin for every rank; the spin's clock rate measured.
+        prof = cupti.KernelProfiler(statsMaxLenPerKernel=8192)
+        prof.initialize()
+        for _ in range(3):  # first windows of a fresh capture: not weighed
+            step(prof)
+        torch.cuda.synchronize()
+        prof.reset()
+        for _ in range(5):
+            step(prof)
+        torch.cuda.synchronize()
+        st = prof.get_stats()
+        # NUM x MED: a kernel whose duration spikes once does not size the spin
+        f_ms = sum(v.num_calls * v.median for v in st.values()) / 5 / 1e3
+        if rank == 0:
+            top = sorted(st.items(), key=lambda kv: -kv[1].num_calls * kv[1].avg)[:3]
+            print("CALIB kernels=%d sum_num_avg_ms=%.3f sum_num_med_ms=%.3f top=%s" % (
+                len(st), sum(v.num_calls * v.avg for v in st.values()) / 5 / 1e3, f_ms,
+                [(k[:40], v.num_calls, round(v.avg, 1), round(v.median, 1)) for k, v in top]))
+        prof.shutdown()
+        prof.close()
         per_ms = 1e6 / gpu_ms(lambda: torch.cuda._sleep(1_000_000), n=3)
         t = torch.tensor([f_ms], dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        base = int(args.spin_ratio * float(t.item()) * per_ms)
+        base = int(args.spin_ratio * min(float(t.item()), 50.0) * per_ms)  # at most 300 ms
         if rank == 0:
-            print(f"SPIN forward_ms={float(t.item()):.3f} spin_cycles={base} cycles_per_ms={per_ms:.0f}")
+            print(f"SPIN forward_kernel_ms={float(t.item()):.3f} spin_cycles={base} "
+                  f"cycles_per_ms={per_ms:.0f}")
     model_.spin = int(base * factor)
-    for _ in range(2):
-        step()
+    step()
     step_ms_base = None
     if args.base_iters > 0:
         torch.cuda.synchronize()

@@ -45,7 +45,7 @@ def test_ddp_slow_rank_is_detected():
 def test_gpt2_ddp_slow_rank_is_detected():
     """the same check on GPT-2 small (12 layers, d=768, ctx 1024, bf16
     autocast, fused AdamW; 2 ranks x 2 x 1024 tokens), rank 1's forward made 1.5x slower by the
-    spin kernel sized to 4x the forward's GPU time (score 5/7 for rank 1, 1 for rank 0).  The
+    spin kernel sized to 6x the forward's GPU time (score 7/10 for rank 1, 1 for rank 0).  The
     forward's hundreds of GEMM / attention / norm launches are captured and scored with it."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -55,12 +55,12 @@ def test_gpt2_ddp_slow_rank_is_detected():
            os.path.join(ROOT, "tests", "func", "ddp_straggler.py"),
            "--model", "gpt2", "--batch", "2", "--seq", "1024", "--iters", "31",
            "--report-iter-interval", "10", "--slow-ranks", "1", "--slow-factor", "1.5",
-           "--spin-ratio", "4", "--base-iters", "5"]
+           "--spin-ratio", "6", "--base-iters", "5"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=480)
     log = r.stdout.splitlines()
     assert r.returncode == 0, r.stderr[-4000:]
     print("\n".join(ln for ln in log if "STRAGGLER" in ln or "perf scores" in ln
-                    or ln.startswith(("STEP MS", "SPIN"))))
+                    or ln.startswith(("STEP MS", "SPIN", "CALIB"))))
     assert any("DONE" in ln for ln in log)
     assert len([ln for ln in log if "STRAGGLER REPORT" in ln]) == 3
     assert _found(log, r"DETECTED RELATIVE STRAGGLER GPU RANK=(\d+)") == {1}

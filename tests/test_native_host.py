@@ -62,8 +62,13 @@ def test_native_host_matches_oracle(tmp_path):
     st = O.matrix_stats(ns, R * K, S, 0, S, cap)
     for f in ("num", "min", "max", "med"):
         assert np.array_equal(g[f].view(np.int32), st[f].view(np.int32)), f
-    for f in ("avg", "std"):  # NVRX_STATS_FAST: the exact mean / std rounded once
-        np.testing.assert_allclose(g[f], st[f], rtol=1e-6, atol=0)
+    # NVRX_STATS_FAST: the exact mean / std rounded once, so within the reference's own f32
+    # accumulation error of it (sequential sums over 1024 samples: ~1.5e-6 seen), and within
+    # one rounding of the exact mean of the retained f32 microsecond values
+    for f in ("avg", "std"):
+        np.testing.assert_allclose(g[f], st[f], rtol=1e-5, atol=0)
+    us = O.ns_to_us(ns.reshape(R * K, S)[:, S - cap:]).astype(np.float64)
+    np.testing.assert_allclose(g["avg"], us.mean(axis=1), rtol=2.5e-7, atol=0)
     gr, gi = O.scores(st["num"].reshape(R, K), st["med"].reshape(R, K), st["avg"].reshape(R, K))
     np.testing.assert_allclose(gpu_rel, gr, rtol=1e-6, atol=0)
     np.testing.assert_allclose(gpu_ind, gi, rtol=1e-6, atol=0)

@@ -1,6 +1,7 @@
 """GPT-2 small (12 layers, d=768, 12 heads, vocab 50257, ctx 1024) as the configs[4] workload
 of tools/live_gpt2.py and tests/func/ddp_straggler.py --model gpt2: random init (no checkpoint
 offline), scaled-dot-product attention, tied head."""
+import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
