@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define NVRX_ABI_VERSION 5
+#define NVRX_ABI_VERSION 6
 
 #define NVRX_OK 0
 #define NVRX_ERR_INVALID -1   /* bad argument / shape */
@@ -352,6 +352,13 @@ typedef struct nvrx_capture_counters {
      * whose own completion signal was chained behind them, and ring records found past their
      * expected value (0 unless the packet processor does not decrement by one) */
     int64_t queues, ring_records, pool_signals, chained_signals, ring_anomalies;
+    /* (ABI 6) queue delivery: dispatches not captured because NVRX_CAPTURE_MAX_PENDING (default
+     * 2^20) dispatches already waited for a harvest, or no completion signal was left -- a profiler
+     * started for a very long time with no stop, get_stats or flush in between.  The reference's
+     * CUPTI buffer pool drops records the same way when every buffer is in use (BufferPool.cpp:44-52);
+     * at every start the library harvests once half the completion ring waits, so a started /
+     * stopped profiler (a detection section per step) never reaches the bound. */
+    int64_t dropped;
 } nvrx_capture_counters;
 int nvrx_capture_stats(nvrx_capture_counters* out);
 

@@ -355,6 +355,17 @@ rocprofiler_tool_configure_result_t* nvrx_tool_configure(uint32_t, const char*, 
     id->name = "nvrx-straggler";
     cap().client = id;
     cap().delivery = parse_delivery();
+    // queue delivery tells the library's own report kernels apart by the thread the intercept
+    // handler runs on, which is the launching thread only under the HIP runtime's direct dispatch
+    // (ADVICE r05): without it, rocprofiler-sdk's dispatch tracing (callback delivery) is used
+    if (cap().delivery == 3) {
+        const char* dd = std::getenv("AMD_DIRECT_DISPATCH");
+        if (dd && std::string(dd) == "0") {
+            std::fprintf(stderr, "nvrx capture: AMD_DIRECT_DISPATCH=0 (packets submitted off the launching "
+                                 "thread); using callback delivery\n");
+            cap().delivery = 1;
+        }
+    }
     if (cap().delivery == 3 &&
         rocprofiler_at_intercept_table_registration(hsa_table_cb, ROCPROFILER_HSA_TABLE, nullptr) !=
             ROCPROFILER_STATUS_SUCCESS) {
@@ -453,6 +464,15 @@ int capture_start(nvrx_profiler* p) {
     c.target.store(p);
     if (c.delivery == 3) {
         ring_setup();  // once, on the first start (this thread may make HIP calls)
+        // a profiler started again and again with no flush in between (a detection section per
+        // step, reports rare) harvests here once half the ring waits, so the ring's records keep
+        // being reused instead of the dispatches falling back to host-memory signals
+        size_t waiting = 0;
+        {
+            std::lock_guard<std::mutex> lk(c.pmu);
+            waiting = c.pending.size();
+        }
+        if (c.ring_n > 0 && waiting > (size_t)c.ring_n / 2) q_harvest(p);
         c.qactive.store(true, std::memory_order_release);
         return 0;
     }
@@ -614,6 +634,7 @@ int nvrx_capture_stats(nvrx_capture_counters* out) {
     out->pool_signals = (int64_t)(c.n_signals.load() - c.n_ring.load());
     out->chained_signals = (int64_t)c.n_chained.load();
     out->ring_anomalies = (int64_t)c.n_ring_bad.load();
+    out->dropped = (int64_t)c.n_dropped.load();
     return NVRX_OK;
 }
 

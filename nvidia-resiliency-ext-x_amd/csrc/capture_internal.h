@@ -101,9 +101,18 @@ struct Capture {
     std::mutex pmu;
     std::vector<Pending> pending;
     std::vector<hsa_signal_t> pool;
+    // bounds: at most max_pending dispatches wait for a harvest (NVRX_CAPTURE_MAX_PENDING,
+    // default 2^20); past it a dispatch goes out without a completion record and counts as dropped,
+    // as the CUPTI buffer pool drops records when every buffer is in use (BufferPool.cpp:44-52).
+    // The pool holds at most kPoolMax signals; a harvest destroys free ones above kPoolKeep.
+    static constexpr size_t kPoolMax = 65536, kPoolKeep = 1024;
+    size_t max_pending = (size_t)1 << 20;
+    size_t pool_total = 0;  // signals created and not destroyed (pmu)
+    std::atomic<uint64_t> n_dropped{0};
     std::atomic<bool> qactive{false};     // the profiler is started
     std::atomic<bool> q_installed{false}; // hsa_queue_create is ours
     std::atomic<uint64_t> n_queues{0}, n_signals{0}, n_signal_fail{0}, n_chained{0};
+    std::atomic<bool> q_table_incomplete{false};  // the HSA table lacked an entry: no queue delivery
     double tick_ns = 0.0;                 // ns per HSA system timestamp tick (first harvest; ring_copy_mu)
     // NVRX_CAPTURE_QUEUE_DIAG (cost attribution only; outputs wrong): 1 = intercept, no signals;
     // 2 = signals on queues without profiling (no timestamps)

@@ -26,6 +26,7 @@ struct QueueFns {
     decltype(hsa_amd_profiling_set_profiler_enabled)* prof_enable = nullptr;
     decltype(hsa_amd_profiling_get_dispatch_time)* dispatch_time = nullptr;
     decltype(hsa_amd_signal_create)* signal_create = nullptr;
+    decltype(hsa_signal_destroy)* signal_destroy = nullptr;
     decltype(hsa_signal_load_scacquire)* load = nullptr;
     decltype(hsa_signal_store_relaxed)* store = nullptr;
     decltype(hsa_system_get_info)* sys_info = nullptr;
@@ -91,15 +92,29 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
                 if (e.slot < 0) c.n_ring_full.fetch_add(1, std::memory_order_relaxed);
                 else c.n_ring.fetch_add(1, std::memory_order_relaxed);
             }
+            if (e.slot >= 0 && c.pending.size() >= c.max_pending) {  // (cannot happen: ring < cap)
+                c.ring_busy[e.slot] = 0;
+                ++c.ring_val[e.slot];
+                e.slot = -1;
+            }
             if (e.slot < 0) {  // an HSA signal of the pool
-                if (c.pool.empty()) {  // grow (rare: the pool keeps what reports returned)
+                if (c.pending.size() >= c.max_pending) {
+                    // started for long without a stop or flush: dropped, not held (bounded memory,
+                    // and no harvest walk over an unbounded list under pmu)
+                    c.n_dropped.fetch_add(1, std::memory_order_relaxed);
+                    ++j;
+                    continue;
+                }
+                if (c.pool.empty() && c.pool_total < Capture::kPoolMax) {  // grow (the pool keeps what reports returned)
                     for (int g = 0; g < 256; ++g) {
                         hsa_signal_t s{0};
                         if (qf.signal_create(1, 0, nullptr, HSA_AMD_SIGNAL_AMD_GPU_ONLY, &s) != HSA_STATUS_SUCCESS) break;
                         c.pool.push_back(s);
+                        ++c.pool_total;
                     }
                 }
                 if (c.pool.empty()) {
+                    c.n_dropped.fetch_add(1, std::memory_order_relaxed);
                     ++j;  // no signal: the packet goes out as it came
                     continue;
                 }
@@ -182,13 +197,23 @@ void hsa_table_cb(rocprofiler_intercept_table_t type, uint64_t, uint64_t, void**
     qf.prof_enable = t->amd_ext_->hsa_amd_profiling_set_profiler_enabled_fn;
     qf.dispatch_time = t->amd_ext_->hsa_amd_profiling_get_dispatch_time_fn;
     qf.signal_create = t->amd_ext_->hsa_amd_signal_create_fn;
+    qf.signal_destroy = t->core_->hsa_signal_destroy_fn;
     qf.load = t->core_->hsa_signal_load_scacquire_fn;
     qf.store = t->core_->hsa_signal_store_relaxed_fn;
     qf.sys_info = t->core_->hsa_system_get_info_fn;
     qf.agent_info = t->core_->hsa_agent_get_info_fn;
     if (!qf.queue_create || !qf.icreate || !qf.iregister || !qf.prof_enable || !qf.dispatch_time ||
-        !qf.signal_create || !qf.load || !qf.store || !qf.sys_info || !qf.agent_info)
+        !qf.signal_create || !qf.signal_destroy || !qf.load || !qf.store || !qf.sys_info || !qf.agent_info) {
+        // too late to fall back to rocprofiler-sdk dispatch tracing (its services are configured in
+        // tool_init, before the runtime hands over this table): capture stays unavailable
+        // (nvrx_profiler_capture_available() == 0) and says so
+        cap().q_table_incomplete = true;
+        std::fprintf(stderr, "nvrx capture: the HSA API table lacks an entry queue delivery needs; kernel "
+                             "dispatches are NOT captured (NVRX_CAPTURE_DELIVERY=callback uses "
+                             "rocprofiler-sdk tracing instead)\n");
         return;
+    }
+    cap().max_pending = (size_t)std::max<int64_t>(1024, env_int("NVRX_CAPTURE_MAX_PENDING", (int64_t)1 << 20));
     cap().qdiag = (int)env_int("NVRX_CAPTURE_QUEUE_DIAG", 0);
     t->core_->hsa_queue_create_fn = q_create;
     cap().q_installed = true;
@@ -389,6 +414,11 @@ void q_harvest(nvrx_profiler* p) {
             if (e.slot >= 0) continue;
             qf.store(e.sig, 1);
             c.pool.push_back(e.sig);
+        }
+        while (c.pool.size() > Capture::kPoolKeep) {  // a burst's signals back to the runtime
+            (void)qf.signal_destroy(c.pool.back());
+            c.pool.pop_back();
+            --c.pool_total;
         }
     }
     c.n_cb.fetch_add(1);

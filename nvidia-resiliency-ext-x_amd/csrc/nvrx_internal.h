@@ -40,7 +40,7 @@ hipError_t section_stats(const double* vals, const int64_t* off, int64_t nsec, i
 hipError_t stragglers(const double* score, int64_t n, double thr, uint8_t* mask, hipStream_t st);
 
 #define NVRX_RECORDS_MAX_LDS (144 * 1024)
-// Stream-ordered device scratch from the default memory pool (segment_ragged.hip): the pool keeps
+// Stream-ordered device scratch from a private memory pool per device (segment_ragged.hip): it keeps
 // up to NVRX_SCRATCH_KEEP_BYTES of freed blocks across synchronisations, so steady-state reports
 // do not return to the driver, while a long-ring report's larger scratch goes back to the job.
 #define NVRX_SCRATCH_KEEP_BYTES ((uint64_t)256 << 20)

@@ -24,23 +24,34 @@
 
 namespace nvrx {
 
-// (nvrx_internal.h) the default pool's release threshold is raised once, to a cap: freed scratch
-// up to NVRX_SCRATCH_KEEP_BYTES stays reserved for the next report; above it (the long-ring
-// paths: up to 4 B per retained sample of the segments in flight) it is released at the next
-// synchronisation instead of staying taken from the training job
+// (nvrx_internal.h) scratch comes from a memory pool of the library's own per device,
+// whose release threshold is capped: freed scratch up to NVRX_SCRATCH_KEEP_BYTES stays reserved for
+// the next report; above it (the long-ring paths: up to 4 B per retained sample of the segments in
+// flight) it is released at the next synchronisation instead of staying taken from the training job.
+// The device's default pool -- PyTorch's hipMallocAsync allocator backend sets its threshold to keep
+// everything -- is left as the job configured it.  Inside a stream capture the allocation is the
+// graph's own node (hipMallocAsync: the graph memory pool).
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipError_t e = hipStreamIsCapturing(st, &cs); e != hipSuccess) return e;
+    if (cs != hipStreamCaptureStatusNone) return hipMallocAsync(p, bytes, st);
     static std::once_flag once[64];
+    static hipMemPool_t pools[64] = {};
     int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        std::call_once(once[dev], [dev] {
-            hipMemPool_t pool;
-            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-                uint64_t thr = NVRX_SCRATCH_KEEP_BYTES;
-                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-            }
-        });
-    }
-    return hipMallocAsync(p, bytes, st);
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipMallocAsync(p, bytes, st);
+    std::call_once(once[dev], [dev] {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t pool = nullptr;
+        if (hipMemPoolCreate(&pool, &props) != hipSuccess) return;  // the default pool then
+        uint64_t thr = NVRX_SCRATCH_KEEP_BYTES;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        pools[dev] = pool;
+    });
+    return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], st) : hipMallocAsync(p, bytes, st);
 }
 
 using namespace ragged;

@@ -13,7 +13,7 @@ import threading
 from typing import Optional
 
 LIB_NAME = "libnvrx_hip.so"
-ABI_VERSION = 5  # include/nvrx_straggler.h NVRX_ABI_VERSION
+ABI_VERSION = 6  # include/nvrx_straggler.h NVRX_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 NVRX_OK = 0
@@ -63,7 +63,8 @@ class CaptureCounters(ctypes.Structure):
                 ("flush_tail_ns", i64), ("enqueues_counted", i64), ("counted_flushes", i64),
                 ("quiet_flushes", i64), ("flush_timeouts", i64), ("owed_abandoned", i64),
                 ("delivery", i32), ("marking", i32), ("queues", i64), ("ring_records", i64),
-                ("pool_signals", i64), ("chained_signals", i64), ("ring_anomalies", i64)]
+                ("pool_signals", i64), ("chained_signals", i64), ("ring_anomalies", i64),
+                ("dropped", i64)]
 
 
 class ProfilerConfig(ctypes.Structure):

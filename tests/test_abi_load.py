@@ -31,7 +31,7 @@ def test_python_binding_covers_header():
 
 def test_lib_loads_and_reports_abi():
     L = _native.lib()
-    assert L.nvrx_abi_version() == _native.ABI_VERSION == 5
+    assert L.nvrx_abi_version() == _native.ABI_VERSION == 6
     cnt = ctypes.c_int(-1)
     # no HIP device in the CPU container: the call succeeds (0 devices) or reports HIP error
     rc = L.nvrx_device_count(ctypes.byref(cnt))
@@ -62,5 +62,5 @@ def test_capture_counters_without_capture():
     assert (c.callbacks, c.dispatches, c.flushes, c.callback_ns) == (0, 0, 0, 0)
     assert (c.enqueues_counted, c.counted_flushes, c.flush_timeouts, c.delivery) == (0, 0, 0, -1)
     # the C struct and the ctypes mirror agree on the layout (two int32 at the end)
-    assert ctypes.sizeof(c) == 16 * 8 + 2 * 4 + 5 * 8
+    assert ctypes.sizeof(c) == 16 * 8 + 2 * 4 + 6 * 8
     assert _native.lib().nvrx_capture_stats(None) == _native.NVRX_ERR_INVALID

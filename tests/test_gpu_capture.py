@@ -111,3 +111,51 @@ def test_dispatch_completing_after_stop_is_captured():
     assert out["pending_at_stop"]
     assert out["strag"] == 7      # enqueued while started, completed after stop
     assert out["after_reset"] == 0
+
+
+BOUND_CHILD = r"""
+import ctypes, json, sys
+sys.path.insert(0, %(pkg)r)
+from nvidia_resiliency_ext.straggler import cupti, ops, _native
+import torch
+p = cupti.KernelProfiler(statsMaxLenPerKernel=8192, capture=True)
+p.initialize()
+score = torch.rand(1000, dtype=torch.float64, device="cuda")
+# started for a long time with no stop or flush: at most NVRX_CAPTURE_MAX_PENDING dispatches wait
+p.start()
+for _ in range(%(n)d):
+    ops.stragglers(score, 0.5)
+torch.cuda.synchronize()
+c = _native.CaptureCounters()
+_native.lib().nvrx_capture_stats(ctypes.byref(c))
+dropped_while_started = c.dropped
+p.stop()
+num = sum(v.num_calls for k, v in p.get_stats().items() if "stragglers" in k)
+p.reset()
+# a section per step (start / stop, no flush): the start-time harvest keeps the ring turning
+for _ in range(%(n)d):
+    p.start()
+    ops.stragglers(score, 0.5)
+    p.stop()
+torch.cuda.synchronize()
+num2 = sum(v.num_calls for k, v in p.get_stats().items() if "stragglers" in k)
+_native.lib().nvrx_capture_stats(ctypes.byref(c))
+print("RESULT " + json.dumps(dict(dropped=dropped_while_started, num=num, num2=num2,
+                                  dropped_after=c.dropped, delivery=c.delivery)))
+"""
+
+
+def test_queue_delivery_pending_bound_drops_and_counts():
+    """a profiler left started never holds more than NVRX_CAPTURE_MAX_PENDING dispatches
+    (the rest go out without a completion record and count as `dropped`, as the reference's buffer
+    pool drops records when it is exhausted, BufferPool.cpp:44-52); with a ring of 2,048 records a
+    start / stop per kernel (harvested at start once half the ring waits) loses nothing."""
+    code = BOUND_CHILD % dict(pkg=os.path.join(ROOT, "nvidia-resiliency-ext-x_amd"), n=3000)
+    env = dict(os.environ, NVRX_CAPTURE_MAX_PENDING="2048", NVRX_CAPTURE_RING="2048")
+    env.pop("NVRX_CAPTURE_DELIVERY", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][7:])
+    assert out["delivery"] == 3
+    assert out["num"] == 2048 and out["dropped"] == 3000 - 2048, out
+    assert out["num2"] == 3000 and out["dropped_after"] == out["dropped"], out
