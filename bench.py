@@ -147,7 +147,7 @@ def timed_pipe_loop(pipe, steps, world, mode="spin"):
 TIMED_REPORTS = 10  # statistics-kernel timing phase after the throughput loop
 # Untimed warm-up runs at least `warmup` reports AND at least this long: MI355X clocks ramp under
 # sustained load, and a timed run that starts after a few milliseconds of work reads ~3 % slower
-# per report at 20 reports (tools/probe_pipeline_fill.py, profiles/r04/pipeline_fill.json)
+# per report at 20 reports (profiles/r04/pipeline_fill.json)
 WARMUP_MIN_MS = 40.0
 
 

@@ -220,7 +220,7 @@ def section():
     ops.stragglers(score, 0.5, out=m)  # the one real kernel: 256 threads, 4 blocks
     # a module kernel through the ext launch (global size in work-items): 1024 over workgroups
     # of 256 = 4 blocks.  (HIP refuses a global size that is not a multiple of the workgroup,
-    # tools/probe_ext_launch.py, so a partial last block -- counted by the capture's ceil, as
+    # (round 4 probe, profiles/r05/README.md 3.6), so a partial last block -- counted by the capture's ceil, as
     # CUPTI's gridX counts it -- cannot be produced through HIP)
     rc = hip.hipExtModuleLaunchKernel(fn, 1024, 1, 1, 256, 1, 1, 0, stream, params, None,
                                       None, None, 0)
@@ -249,7 +249,7 @@ def test_runtime_copies_and_fills_are_not_kernels():
     global size in work-items) yields exactly the two kernels' keys (:182-185).  The capture's
     grid dims are ceil(grid_size / workgroup_size), as CUPTI's gridX counts a partial last block;
     that ceil branch cannot be reached through HIP (it refuses a global size that is not a
-    multiple of the workgroup, tools/probe_ext_launch.py), so only whole blocks are exercised."""
+    multiple of the workgroup, round 4 probe), so only whole blocks are exercised."""
     assert os.path.exists(PROBE), "build tests/native first (__graft_entry__.build())"
     out = _child(RUNTIME)
     assert out["available"]
