@@ -620,6 +620,9 @@ def main():
                           f"restatement",
                    gpu_stats_bit_exact_on_sample=cb["parity"])
 
+    # (collectives: on every rank, before rank 0 writes the line)
+    ms_bounded = (comm_max(r["elapsed_bounded"], world, dev) / args.steps * 1e3
+                  if r.get("elapsed_bounded") is not None else None)
     if rank == 0:
         # the committed PMC pass is of the 1-GPU launch (64 x 2048 segments); a shard of
         # 2048*N hashed kernels has a different size, so its traffic is not claimed
@@ -639,8 +642,7 @@ def main():
             # the timed loop's host waits poll (batch.set_sync_mode("spin")); the batch API's
             # default waits poll at most 50 us, then block -- the same loop in that mode:
             "host_wait": "spin", "inputs_in_flight": INPUTS_IN_FLIGHT,
-            "ms_per_step_bounded_wait": (comm_max(r["elapsed_bounded"], world, dev) / args.steps * 1e3
-                                         if r.get("elapsed_bounded") is not None else None),
+            "ms_per_step_bounded_wait": ms_bounded,
             "graph_phases": phases,
             "higher_is_better": True,
             "scaling": "weak",
