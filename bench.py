@@ -125,6 +125,17 @@ INPUTS_IN_FLIGHT = 2
 SEED_ALT = synth.SEED ^ 0x5A5A5A5A
 
 
+def on_first_input(pipe):
+    """One more (untimed) report at a time until one reads the first input set: the result the
+    legs report (straggler sets, the strong-scaled legs' score digest compared across N) is then
+    the same input's on every N, whatever the warm-up count was."""
+    while True:
+        pipe.submit()
+        res, _ = pipe.collect()
+        if pipe.last_input == 0:
+            return res
+
+
 def timed_pipe_loop(pipe, steps, world, mode="spin"):
     """`steps` back-to-back reports, two in flight, between barriers, with the host waiting in
     the given sync mode (batch.SYNC_MODES).  Returns (last result, elapsed s)."""
@@ -244,6 +255,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
                 res_t, ms = pipe.collect()
                 ks.append(ms)
             barrier(world)
+        res = on_first_input(pipe)
         keep = min(s_push, cap)
         phases = None
         if graph_phases:
@@ -332,6 +344,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     for _ in range(TIMED_REPORTS):
         pipe.submit(timed=True)
         ks.append(pipe.collect()[1])
+    res = on_first_input(pipe)
     stats_ms = comm_max(float(np.mean(ks)), world, dev)
     launch = pipe_label(pipe)
     tmax = allreduce(elapsed, torch.distributed.ReduceOp.MAX if world > 1 else None, world, dev)

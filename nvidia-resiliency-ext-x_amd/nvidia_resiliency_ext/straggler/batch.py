@@ -661,6 +661,7 @@ class PipelinedReports:
         self.pending = []  # (slot, timed) in flight, oldest first
         self.ready = []    # results collected early (a timed submit drains), oldest first
         self.n = 0
+        self.last_input = None
         rep._pipes.add(self)
 
     def submit(self, timed: bool = False) -> None:
@@ -748,6 +749,7 @@ class PipelinedReports:
         wait_event(ev)
         if self.alt:  # the caller's later work (new inputs, the history) follows this report
             torch.cuda.current_stream(self.rep.device).wait_event(ev)
+        self.last_input = k % len(self.inputs)  # the input set the collected report read
         now = [t._version for t in self.inputs[k % len(self.inputs)]]
         if now != self._versions[k]:
             raise RuntimeError("PipelinedReports: an input of this report was modified in place "
