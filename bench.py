@@ -250,10 +250,14 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         # reports submitted on an idle device with HIP events around the statistics phase
         ks = []
         if time_kernel:
+            # host waits poll here too: a host just woken from a blocking wait queues the graph
+            # after the pre-roll spin has ended, and the first event would time that gap
+            prev = batch.set_sync_mode("spin")
             for _ in range(TIMED_REPORTS):
                 pipe.submit(timed=True)
                 res_t, ms = pipe.collect()
                 ks.append(ms)
+            batch.set_sync_mode(prev)
             barrier(world)
         res = on_first_input(pipe)
         keep = min(s_push, cap)
@@ -341,9 +345,11 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     warm_pipelined(pipe, warmup, world)
     res, elapsed = timed_pipe_loop(pipe, steps, world, "spin")
     ks = []
+    prev = batch.set_sync_mode("spin")  # as run_config's timed reports
     for _ in range(TIMED_REPORTS):
         pipe.submit(timed=True)
         ks.append(pipe.collect()[1])
+    batch.set_sync_mode(prev)
     res = on_first_input(pipe)
     stats_ms = comm_max(float(np.mean(ks)), world, dev)
     launch = pipe_label(pipe)
