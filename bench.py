@@ -156,6 +156,7 @@ def timed_pipe_loop(pipe, steps, world, mode="spin"):
 
 
 TIMED_REPORTS = 10  # statistics-kernel timing phase after the throughput loop
+TIMED_REPS = 4      # statistics replays back to back per timed report (events around all four)
 # Untimed warm-up runs at least `warmup` reports AND at least this long: MI355X clocks ramp under
 # sustained load, and a timed run that starts after a few milliseconds of work reads ~3 % slower
 # per report at 20 reports (profiles/r04/pipeline_fill.json)
@@ -254,7 +255,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
             # after the pre-roll spin has ended, and the first event would time that gap
             prev = batch.set_sync_mode("spin")
             for _ in range(TIMED_REPORTS):
-                pipe.submit(timed=True)
+                pipe.submit(timed=True, reps=TIMED_REPS)
                 res_t, ms = pipe.collect()
                 ks.append(ms)
             batch.set_sync_mode(prev)
@@ -347,7 +348,7 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     ks = []
     prev = batch.set_sync_mode("spin")  # as run_config's timed reports
     for _ in range(TIMED_REPORTS):
-        pipe.submit(timed=True)
+        pipe.submit(timed=True, reps=TIMED_REPS)
         ks.append(pipe.collect()[1])
     batch.set_sync_mode(prev)
     res = on_first_input(pipe)
@@ -688,10 +689,11 @@ def main():
                          # the same bytes over the pipelined loop's time per report (two reports'
                          # statistics kernels overlap at their boundaries)
                          "per_report_frac": alg_bytes / (ms_per_step * 1e-3) / HBM_PEAK,
-                         "kernel_ms_is": "the statistics kernel timed alone on an idle device (HIP "
-                                         "events, after the loop); in the loop two reports' kernels "
-                                         "overlap at their launch boundaries, so ms_per_step can be "
-                                         "below it"},
+                         "kernel_ms_is": "the statistics kernel on an idle device after the loop: "
+                                         "HIP events on its stream around 4 back-to-back replays, "
+                                         "10 reports, mean per replay; in the loop two reports' "
+                                         "kernels overlap at their launch boundaries, so "
+                                         "ms_per_step can be below it"},
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,
             "configs0_report": c1,

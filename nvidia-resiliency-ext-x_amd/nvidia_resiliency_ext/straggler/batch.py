@@ -555,7 +555,10 @@ class PipelinedReports:
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
-    statistics kernel on an otherwise idle device, for a sample of the reports.
+    statistics kernel on an otherwise idle device, for a sample of the reports; submit(timed=True,
+    reps=n) replays the statistics phase n times back to back between the events (the same inputs
+    and outputs each time) and collect() returns the mean per replay, so the events' own overhead
+    is spread over n launches.
     stats: the statistics phase as a callable, or a list of them, one per input set (report i
     runs stats[i % len(stats)]; default: compute_stats(ns, s_push); record streams:
     MatrixReporter.pipelined_records).  inputs: per input set, the tensors its statistics phase
@@ -664,8 +667,10 @@ class PipelinedReports:
         self.last_input = None
         rep._pipes.add(self)
 
-    def submit(self, timed: bool = False) -> None:
+    def submit(self, timed: bool = False, reps: int = 1) -> None:
         """Queue the next report (at most `depth` in flight: collect() the oldest first)."""
+        if reps < 1 or (reps > 1 and not timed):
+            raise ValueError("reps: a timed report's statistics replays (>= 1)")
         if len(self.pending) == self.depth:
             raise RuntimeError(f"{self.depth} reports in flight: collect() one first")
         if self._needs_clean and not self.rep._colref_clean:
@@ -707,7 +712,8 @@ class PipelinedReports:
             with torch.cuda.stream(s):
                 if timed:
                     self.ev[0].record(s)
-                self.stats_g[k].replay()
+                for _ in range(reps):
+                    self.stats_g[k].replay()
                 if timed:
                     self.ev[1].record(s)
             self.stats_done[k].record(s)
@@ -731,7 +737,8 @@ class PipelinedReports:
         else:
             if timed:
                 self.ev[0].record()
-                self.stats.replay()
+                for _ in range(reps):
+                    self.stats.replay()
                 self.ev[1].record()
                 self.rest[k].replay()
             else:
@@ -740,7 +747,7 @@ class PipelinedReports:
         self.rep._colref_clean = self.rep._fuse_ref()
         if not self.pending:
             self._burst = self.n  # the first report of a burst (submitted to an empty pipeline)
-        self.pending.append((k, timed))
+        self.pending.append((k, reps if timed else 0))
         self.n += 1
 
     def _land(self):
@@ -755,7 +762,7 @@ class PipelinedReports:
             raise RuntimeError("PipelinedReports: an input of this report was modified in place "
                                "while the report was in flight (submit() -> collect()); its "
                                "results are undefined -- modify inputs only after collect()")
-        ms = self.ev[0].elapsed_time(self.ev[1]) if timed else None
+        ms = self.ev[0].elapsed_time(self.ev[1]) / timed if timed else None  # timed = replays
         return self.rep._unpack(self.bufs[k]), ms
 
     def collect(self):
