@@ -156,7 +156,7 @@ def timed_pipe_loop(pipe, steps, world, mode="spin"):
 
 
 TIMED_REPORTS = 10  # statistics-kernel timing phase after the throughput loop
-TIMED_REPS = 4      # statistics replays back to back per timed report (events around all four)
+TIMED_REPS = 4      # statistics phases back to back in one graph per timed report (events around it)
 # Untimed warm-up runs at least `warmup` reports AND at least this long: MI355X clocks ramp under
 # sustained load, and a timed run that starts after a few milliseconds of work reads ~3 % slower
 # per report at 20 reports (profiles/r04/pipeline_fill.json)
@@ -242,7 +242,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
         # nothing but back-to-back reports.  N GPUs: per report statistics, the shard's partials
         # and the combine as graphs, the all_gather of the partials eager between them
         ns_alt, _ = make_shard(R, K_global, s_push, world, rank, dev, seed=SEED_ALT)
-        pipe = rep.pipelined([ns, ns_alt], s_push, timing=time_kernel)
+        pipe = rep.pipelined([ns, ns_alt], s_push, timing=time_kernel, timing_reps=TIMED_REPS)
         warm_pipelined(pipe, warmup, world)
         res, elapsed = timed_pipe_loop(pipe, steps, world, "spin")
         # the same loop with the API's default host wait (bounded spin, then block)
@@ -255,7 +255,7 @@ def run_config(cfg, K_global, steps, warmup, world, rank, dev, time_kernel=True,
             # after the pre-roll spin has ended, and the first event would time that gap
             prev = batch.set_sync_mode("spin")
             for _ in range(TIMED_REPORTS):
-                pipe.submit(timed=True, reps=TIMED_REPS)
+                pipe.submit(timed=True)
                 res_t, ms = pipe.collect()
                 ks.append(ms)
             batch.set_sync_mode(prev)
@@ -342,13 +342,13 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     # reports two in flight on two streams, each on its own record set, as the headline
     # (MatrixReporter.pipelined_records; N GPUs: statistics, partials and combine as graphs, the
     # all_gather eager between them); the statistics phase timed afterwards on an idle device
-    pipe = rep.pipelined_records([recs, recs_alt], rec_off, timing=True)
+    pipe = rep.pipelined_records([recs, recs_alt], rec_off, timing=True, timing_reps=TIMED_REPS)
     warm_pipelined(pipe, warmup, world)
     res, elapsed = timed_pipe_loop(pipe, steps, world, "spin")
     ks = []
     prev = batch.set_sync_mode("spin")  # as run_config's timed reports
     for _ in range(TIMED_REPORTS):
-        pipe.submit(timed=True, reps=TIMED_REPS)
+        pipe.submit(timed=True)
         ks.append(pipe.collect()[1])
     batch.set_sync_mode(prev)
     res = on_first_input(pipe)
@@ -690,7 +690,8 @@ def main():
                          # statistics kernels overlap at their boundaries)
                          "per_report_frac": alg_bytes / (ms_per_step * 1e-3) / HBM_PEAK,
                          "kernel_ms_is": "the statistics kernel on an idle device after the loop: "
-                                         "HIP events on its stream around 4 back-to-back replays, "
+                                         "HIP events on its stream around one graph of 4 back-to-back "
+                                         "statistics phases, "
                                          "10 reports, mean per replay; in the loop two reports' "
                                          "kernels overlap at their launch boundaries, so "
                                          "ms_per_step can be below it"},

@@ -316,7 +316,8 @@ class MatrixReporter:
         return ReportGraph(self, None, 0, stats=lambda: self.compute_stats_records(recs, rec_off))
 
     def pipelined(self, ns, s_push: int, timing: bool = False,
-                  mode: Optional[str] = None, depth: int = 2) -> "PipelinedReports":
+                  mode: Optional[str] = None, depth: int = 2,
+                  timing_reps: int = 1) -> "PipelinedReports":
         """Reports replayed two deep: report i+1's device work is queued before report i's
         results are read on the host, each report landing in its own pinned buffer (N GPUs: the
         partials exchange of each report stays an eager collective, issued in report order).
@@ -326,6 +327,7 @@ class MatrixReporter:
         changed it (its version counter moved) between that report's submit() and collect()."""
         ins = list(ns) if isinstance(ns, (list, tuple)) else [ns]
         return PipelinedReports(self, None, s_push, timing, mode=mode, depth=depth,
+                                timing_reps=timing_reps,
                                 stats=[lambda x=x: self.compute_stats(x, s_push) for x in ins],
                                 stats_bytes=self._matrix_bytes(s_push), inputs=[(x,) for x in ins])
 
@@ -333,14 +335,15 @@ class MatrixReporter:
         keep = min(s_push, self.cap) if self.cap > 0 else s_push
         return 4 * self.R * self.K * keep  # 4 B per retained sample
 
-    def pipelined_records(self, recs, rec_off: torch.Tensor,
-                          timing: bool = False, mode: Optional[str] = None) -> "PipelinedReports":
+    def pipelined_records(self, recs, rec_off: torch.Tensor, timing: bool = False,
+                          mode: Optional[str] = None, timing_reps: int = 1) -> "PipelinedReports":
         """pipelined() over record streams resident in HBM (compute_stats_records: bucketing,
         classification and the class kernels -- side-stream fork / join and stream-ordered
         scratch included -- captured into the report graphs).  recs: one record tensor or a list
         of them (same layout, rec_off shared), as ns for pipelined()."""
         ins = list(recs) if isinstance(recs, (list, tuple)) else [recs]
         return PipelinedReports(self, None, 0, timing, mode=mode, stats_bytes=8 * ins[0].shape[0],
+                                timing_reps=timing_reps,
                                 stats=[lambda r=r: self.compute_stats_records(r, rec_off) for r in ins],
                                 inputs=[(r, rec_off) for r in ins])
 
@@ -555,10 +558,10 @@ class PipelinedReports:
     timing: submit(timed=True) first lets the reports in flight finish, then replays the
     statistics phase as its own graph between two timing events (ROCm's torch refuses events
     inside a capture) and the rest of the report as another -- a clean measurement of the
-    statistics kernel on an otherwise idle device, for a sample of the reports; submit(timed=True,
-    reps=n) replays the statistics phase n times back to back between the events (the same inputs
-    and outputs each time) and collect() returns the mean per replay, so the events' own overhead
-    is spread over n launches.
+    statistics kernel on an otherwise idle device, for a sample of the reports.  timing_reps=n: that
+    graph holds the statistics phase n times back to back (same inputs and outputs each time) and
+    collect() returns the mean per phase, so the events' own overhead and a graph launch are spread
+    over n phases.
     stats: the statistics phase as a callable, or a list of them, one per input set (report i
     runs stats[i % len(stats)]; default: compute_stats(ns, s_push); record streams:
     MatrixReporter.pipelined_records).  inputs: per input set, the tensors its statistics phase
@@ -570,6 +573,7 @@ class PipelinedReports:
 
     def __init__(self, rep: MatrixReporter, ns: Optional[torch.Tensor], s_push: int,
                  timing: bool = False, stats=None, mode: Optional[str] = None,
+                 timing_reps: int = 1,
                  stats_bytes: Optional[int] = None, depth: int = 2, inputs=None):
         self.mode = mode or _PIPE_MODE or "auto"
         if stats_bytes is None:  # the matrix path: 4 B per retained sample
@@ -600,6 +604,9 @@ class PipelinedReports:
             raise ValueError("pipelined reports: depth >= 2 (> 2 with two streams only)")
         self.depth = depth
         self.rep, self.timing = rep, timing
+        if timing_reps < 1:
+            raise ValueError("timing_reps >= 1")
+        self.timing_reps = timing_reps
         self.bufs = [torch.zeros_like(rep.h_out).pin_memory() for _ in range(depth)]
 
         def scores(k: int):
@@ -612,10 +619,14 @@ class PipelinedReports:
             else:
                 rep.compute_scores(out_buf=self.bufs[k])
 
-        def capture(with_stats: bool, rest: bool, k: int):
+        def capture(with_stats: bool, rest: bool, k: int, reps: int = 1):
             g = torch.cuda.CUDAGraph()
+            ready = rep._colref_clean
             with torch.cuda.graph(g):
-                if with_stats:
+                for i in range(reps if with_stats else 0):
+                    # a repeated phase reads the same inputs: the fused reference the previous one
+                    # left is the same minimum, so it needs no re-initialisation either
+                    rep._colref_clean = ready
                     stats[k % len(stats)]()
                 if rest:
                     scores(k)
@@ -629,11 +640,15 @@ class PipelinedReports:
 
         if self.alt:
             self.slots = [_Slot(rep, True)] + [_Slot(rep, False) for _ in range(depth - 1)]
-            self.stats_g, self.rest_g, self.part_g, self.fin_g = [], [], [], []
+            self.stats_g, self.rest_g, self.part_g, self.fin_g, self.stats_t = [], [], [], [], []
             for k, slot in enumerate(self.slots):
                 with slot.bind(rep):
                     _warm_up(rep, stats[k % len(stats)])  # initialises this slot's column reference too
+                    ready = rep._colref_clean
                     self.stats_g.append(capture(True, False, k))
+                    if timing:  # the timed statistics phase, timing_reps times in one graph,
+                        rep._colref_clean = ready  # replacing stats_g in a timed report
+                        self.stats_t.append(capture(True, False, k, self.timing_reps))
                     if rep.exchange:  # N GPUs: partials | eager all_gather | combine + result copy
                         self.part_g.append(capture_fn(rep._scores_partials))
                         self.fin_g.append(capture_fn(lambda k=k: (
@@ -649,7 +664,7 @@ class PipelinedReports:
             self._needs_clean = rep._colref_clean  # as ReportGraph: every graph here pairs both phases
             self.full = [capture(True, True, k) for k in range(2)]
             if timing:
-                self.stats = capture(True, False, 0)
+                self.stats = capture(True, False, 0, self.timing_reps)
                 self.rest = [capture(False, True, k) for k in range(2)]
         if timing:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -667,10 +682,8 @@ class PipelinedReports:
         self.last_input = None
         rep._pipes.add(self)
 
-    def submit(self, timed: bool = False, reps: int = 1) -> None:
+    def submit(self, timed: bool = False) -> None:
         """Queue the next report (at most `depth` in flight: collect() the oldest first)."""
-        if reps < 1 or (reps > 1 and not timed):
-            raise ValueError("reps: a timed report's statistics replays (>= 1)")
         if len(self.pending) == self.depth:
             raise RuntimeError(f"{self.depth} reports in flight: collect() one first")
         if self._needs_clean and not self.rep._colref_clean:
@@ -712,8 +725,7 @@ class PipelinedReports:
             with torch.cuda.stream(s):
                 if timed:
                     self.ev[0].record(s)
-                for _ in range(reps):
-                    self.stats_g[k].replay()
+                (self.stats_t[k] if timed else self.stats_g[k]).replay()
                 if timed:
                     self.ev[1].record(s)
             self.stats_done[k].record(s)
@@ -737,8 +749,7 @@ class PipelinedReports:
         else:
             if timed:
                 self.ev[0].record()
-                for _ in range(reps):
-                    self.stats.replay()
+                self.stats.replay()
                 self.ev[1].record()
                 self.rest[k].replay()
             else:
@@ -747,7 +758,7 @@ class PipelinedReports:
         self.rep._colref_clean = self.rep._fuse_ref()
         if not self.pending:
             self._burst = self.n  # the first report of a burst (submitted to an empty pipeline)
-        self.pending.append((k, reps if timed else 0))
+        self.pending.append((k, self.timing_reps if timed else 0))
         self.n += 1
 
     def _land(self):

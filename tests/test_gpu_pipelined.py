@@ -16,7 +16,8 @@ def test_pipelined_matches_sequential_reports():
     a = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
     b = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
     ns = torch.empty_like(seqs[0])
-    pipe = b.pipelined(ns, S, timing=True)
+    # (timing_reps: a timed report's statistics phase runs three times back to back: same results)
+    pipe = b.pipelined(ns, S, timing=True, timing_reps=3)
     # (no reset_history: the warm-up pass of the capture leaves the individual history as it
     # was, ADVICE r03 -- ns holds uninitialised memory here)
     want, got = [], []
@@ -26,8 +27,7 @@ def test_pipelined_matches_sequential_reports():
     # b: the same five reports, two in flight; the input changes only between collections
     for i in range(5):
         ns.copy_(seqs[i % 2])
-        # (timed reports replay their statistics phase three times back to back: same results)
-        pipe.submit(timed=i % 2 == 0, reps=3 if i % 2 == 0 else 1)
+        pipe.submit(timed=i % 2 == 0)
         res, ms = pipe.collect()
         assert (ms is not None and ms > 0.0) if i % 2 == 0 else ms is None
         got.append(res)
@@ -115,11 +115,11 @@ def test_pipelined_records_matches_eager_reports(R):
     b = batch.MatrixReporter(R, K, cap=cap, thr_rel=0.8, thr_ind=0.8)
     want = [a.report_records(streams[i % 2], rec_off) for i in range(5)]
     recs = torch.empty_like(streams[0])
-    pipe = b.pipelined_records(recs, rec_off, timing=True)
+    pipe = b.pipelined_records(recs, rec_off, timing=True, timing_reps=2)
     got = []
     for i in range(5):
         recs.copy_(streams[i % 2])
-        pipe.submit(timed=i == 2, reps=2 if i == 2 else 1)
+        pipe.submit(timed=i == 2)
         res, ms = pipe.collect()
         assert (ms is not None and ms > 0.0) if i == 2 else ms is None
         got.append(res)
