@@ -73,6 +73,13 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
         uint64_t j = 0;
         for (uint64_t i = 0; i < n; ++i) {
             if (packet_type(in[i].header) != HSA_PACKET_TYPE_KERNEL_DISPATCH) continue;
+            if (c.pending.size() >= c.max_pending) {
+                // started for long without a stop or flush: dropped, not held (bounded memory, and
+                // no harvest walk over an unbounded list under pmu); the packet goes out as it came
+                c.n_dropped.fetch_add(1, std::memory_order_relaxed);
+                ++j;
+                continue;
+            }
             const hsa_kernel_dispatch_packet_t& k = in[i];
             Capture::Pending e{hsa_signal_t{0}, data, k.kernel_object, k.workgroup_size_x, k.workgroup_size_y,
                                k.workgroup_size_z, k.grid_size_x, k.grid_size_y, k.grid_size_z, -1, 0, 0};
@@ -92,19 +99,7 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
                 if (e.slot < 0) c.n_ring_full.fetch_add(1, std::memory_order_relaxed);
                 else c.n_ring.fetch_add(1, std::memory_order_relaxed);
             }
-            if (e.slot >= 0 && c.pending.size() >= c.max_pending) {  // (cannot happen: ring < cap)
-                c.ring_busy[e.slot] = 0;
-                ++c.ring_val[e.slot];
-                e.slot = -1;
-            }
             if (e.slot < 0) {  // an HSA signal of the pool
-                if (c.pending.size() >= c.max_pending) {
-                    // started for long without a stop or flush: dropped, not held (bounded memory,
-                    // and no harvest walk over an unbounded list under pmu)
-                    c.n_dropped.fetch_add(1, std::memory_order_relaxed);
-                    ++j;
-                    continue;
-                }
                 if (c.pool.empty() && c.pool_total < Capture::kPoolMax) {  // grow (the pool keeps what reports returned)
                     for (int g = 0; g < 256; ++g) {
                         hsa_signal_t s{0};
