@@ -14,7 +14,7 @@ sizes the fast ranks' spin to r x the forward's kernel time per step as the dete
 (sum of NUM x AVG over the captured forward kernels, the largest over ranks), so
 that the spin carries a known share of the NUM*AVG weights whatever the model: with forward
 time F and spin rF, a rank slowed s-fold scores (F + rF) / (F + s rF) (reporting.py:219-253),
-0.7 at r = 6, s = 1.5.  Launched with torch.distributed.run; gloo process group, all ranks on
+0.69 at r = 10, s = 1.5.  Launched with torch.distributed.run; gloo process group, all ranks on
 GPU LOCAL_RANK % device_count.  Prints the step time without and with the detector."""
 import argparse
 import os

@@ -45,8 +45,11 @@ def test_ddp_slow_rank_is_detected():
 def test_gpt2_ddp_slow_rank_is_detected():
     """the same check on GPT-2 small (12 layers, d=768, ctx 1024, bf16
     autocast, fused AdamW; 2 ranks x 2 x 1024 tokens), rank 1's forward made 1.5x slower by the
-    spin kernel sized to 6x the forward's GPU time (score 7/10 for rank 1, 1 for rank 0).  The
-    forward's hundreds of GEMM / attention / norm launches are captured and scored with it."""
+    spin kernel sized to 10x the forward's captured kernel time (score 11/16 for rank 1, 1 for rank
+    0; still below the 0.8 threshold SURVEY 8(d) sets should the model kernels' NUM x AVG weigh
+    five times their NUM x MED, as duration spikes from the other process's time slices can make
+    them on a shared GPU).  The forward's GEMM / attention / norm launches are captured and
+    scored with it."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -55,7 +58,7 @@ def test_gpt2_ddp_slow_rank_is_detected():
            os.path.join(ROOT, "tests", "func", "ddp_straggler.py"),
            "--model", "gpt2", "--batch", "2", "--seq", "1024", "--iters", "31",
            "--report-iter-interval", "10", "--slow-ranks", "1", "--slow-factor", "1.5",
-           "--spin-ratio", "6", "--base-iters", "5"]
+           "--spin-ratio", "10", "--base-iters", "5", "--threshold", "0.8"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=480)
     log = r.stdout.splitlines()
     assert r.returncode == 0, r.stderr[-4000:]
