@@ -643,6 +643,8 @@ def main():
     # (collectives: on every rank, before rank 0 writes the line)
     ms_bounded = (comm_max(r["elapsed_bounded"], world, dev) / args.steps * 1e3
                   if r.get("elapsed_bounded") is not None else None)
+    sets_bounded = (all_ranks(r["sets_bounded_ok"] and sets_ok, world, dev)
+                    if "sets_bounded_ok" in r else None)
     if rank == 0:
         # the committed PMC pass is of the 1-GPU launch (64 x 2048 segments); a shard of
         # 2048*N hashed kernels has a different size, so its traffic is not claimed
@@ -700,6 +702,7 @@ def main():
             "configs0_report": c1,
             "zipf_16384_ranks": zipf,
             "straggler_sets_exact": sets_ok,
+            "straggler_sets_exact_bounded_wait": sets_bounded,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
