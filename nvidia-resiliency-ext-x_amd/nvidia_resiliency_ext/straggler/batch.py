@@ -676,7 +676,7 @@ class PipelinedReports:
         frac = float(os.environ.get("NVRX_PIPE_STAGGER", STAGGER_FRAC))
         self.stagger_cycles = int(frac * stats_bytes / 6.5e12 * 2.2e9) if stats_bytes else 0
         self._burst = -2
-        self.pending = []  # (slot, timed) in flight, oldest first
+        self.pending = []  # (slot, statistics phases timed or 0) in flight, oldest first
         self.ready = []    # results collected early (a timed submit drains), oldest first
         self.n = 0
         self.last_input = None
@@ -762,7 +762,7 @@ class PipelinedReports:
         self.n += 1
 
     def _land(self):
-        k, timed = self.pending.pop(0)
+        k, timed = self.pending.pop(0)  # timed: the timed statistics phases (0: untimed)
         ev = self.done[k]
         wait_event(ev)
         if self.alt:  # the caller's later work (new inputs, the history) follows this report
@@ -773,7 +773,7 @@ class PipelinedReports:
             raise RuntimeError("PipelinedReports: an input of this report was modified in place "
                                "while the report was in flight (submit() -> collect()); its "
                                "results are undefined -- modify inputs only after collect()")
-        ms = self.ev[0].elapsed_time(self.ev[1]) / timed if timed else None  # timed = replays
+        ms = self.ev[0].elapsed_time(self.ev[1]) / timed if timed else None
         return self.rep._unpack(self.bufs[k]), ms
 
     def collect(self):
