@@ -394,6 +394,61 @@ def run_zipf(steps, warmup, world, rank, dev, cpu_ranks, threads):
     return out
 
 
+def run_dropin_api(dev, n_reports=50, K=2048, nsec=3):
+    """The drop-in API itself at K = 2048 kernels: one rank's ReportGenerator.generate_report
+    (reporting.py:421-554) on the summaries a Detector hands over -- what a training job pays per
+    report per process.  Against it: the same inputs through the CPU Python restatement of the
+    reference's ReportGenerator (oracle/oracle_report.py, timed the same way) and the reference
+    itself, 13.6 ms per report at ws = 1, K = 2048 in the survey container."""
+    from nvidia_resiliency_ext.straggler import Statistic, reporting
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_report as OR
+
+    rng = np.random.default_rng(7)
+    names = synth.kernel_names(K)
+    num = rng.integers(1, 8193, K)
+    med = (rng.integers(2_000, 2_000_000, K) / np.float32(1000.0)).astype(np.float32)
+    avg = (med * np.float32(1.02)).astype(np.float32)
+    smed = rng.uniform(5.0, 50.0, nsec)
+
+    def summaries(keys, jitter):
+        kk = {n: {keys["MIN"]: float(m * 0.9), keys["MAX"]: float(m * 1.2), keys["MED"]: float(m * jitter),
+                  keys["AVG"]: float(a * jitter), keys["STD"]: float(m * 0.05), keys["NUM"]: int(c)}
+              for n, m, a, c in zip(names, med, avg, num)}
+        ss = {f"section_{i}": {keys["MIN"]: m * 0.9, keys["MAX"]: m * 1.1, keys["MED"]: m * jitter,
+                               keys["AVG"]: m * jitter, keys["STD"]: 0.1, keys["NUM"]: 100}
+              for i, m in enumerate(smed)}
+        return ss, kk
+
+    enum_keys = {k: getattr(Statistic, k) for k in ("MIN", "MAX", "MED", "AVG", "STD", "NUM")}
+    str_keys = {k: k for k in enum_keys}
+    jit = [1.0 + 0.01 * (i % 7) for i in range(n_reports + 1)]
+    gpu_in = [summaries(enum_keys, j) for j in jit]
+    cpu_in = [summaries(str_keys, j) for j in jit]
+    scores = ["relative_perf_scores", "individual_perf_scores"]
+    gen = reporting.ReportGenerator(scores_to_compute=scores, gather_on_rank0=True)
+    sim = OR.SimWorld(1, scores, gather_on_rank0=True)
+    t0 = time.perf_counter()
+    gen.generate_report(*gpu_in[0])  # the first report assigns the name ids
+    first_ms = (time.perf_counter() - t0) * 1e3
+    sim.generate_report([cpu_in[0][0]], [cpu_in[0][1]])
+    t0 = time.perf_counter()
+    for ss, kk in gpu_in[1:]:
+        rep = gen.generate_report(ss, kk)
+    gpu_ms = (time.perf_counter() - t0) / n_reports * 1e3
+    t0 = time.perf_counter()
+    for ss, kk in cpu_in[1:]:
+        want = sim.generate_report([ss], [kk])[0]
+    cpu_ms = (time.perf_counter() - t0) / n_reports * 1e3
+    match = all(abs(getattr(rep, f)[0] - want[f][0]) <= 1e-6 * abs(want[f][0])  # (f32-rounded)
+                for f in ("gpu_relative_perf_scores", "gpu_individual_perf_scores"))
+    return dict(kernels=K, sections=nsec, world_size=1, reports=n_reports,
+                gpu_ms_per_report=gpu_ms, first_report_ms=first_ms,
+                report_elapsed_field_ms=rep.generate_report_elapsed_time,
+                cpu_python_restatement_ms_per_report=cpu_ms,
+                reference_survey_ms_per_report=13.6, scores_match_restatement=match)
+
+
 def cpu_threads() -> int:
     """Host threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, 16 on the GPU
     boxes), never more than this process may run on."""
@@ -625,6 +680,9 @@ def main():
                   gpu_relative_matches_cpu=bool(np.allclose(r1["res"].gpu_relative, gr1, rtol=1e-6)))
         del r1
 
+    # ---------------- the drop-in ReportGenerator at 2048 kernels (rank 0, N == 1) -------
+    api = run_dropin_api(dev) if world == 1 and rank == 0 and not args.no_cpu_baseline else None
+
     # ---------------- CPU baseline (rank 0, N == 1 only) ------------------------------
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -700,6 +758,7 @@ def main():
             "cpu_baseline": cpu,
             "latency_4096_ranks": lat,
             "configs0_report": c1,
+            "dropin_report_2048_kernels": api,
             "zipf_16384_ranks": zipf,
             "straggler_sets_exact": sets_ok,
             "straggler_sets_exact_bounded_wait": sets_bounded,
