@@ -26,8 +26,13 @@ class NameMapper:
         s = self.section_name_to_id
         return all(n in k for n in kernel_names) and all(n in s for n in section_names)
 
-    def gather_and_assign_ids(self, kernel_names: List[str], section_names: List[str]) -> None:
-        if is_all_true(self._check_if_has_all_names(kernel_names, section_names), self.group):
+    def gather_and_assign_ids(self, kernel_names: List[str], section_names: List[str],
+                              kernels_known: bool = False) -> None:
+        """kernels_known: the caller knows every kernel name already has an id (the same names as
+        its previous call), so only the sections are looked up; the collective is unchanged."""
+        have = (all(n in self.section_name_to_id for n in section_names) if kernels_known else
+                self._check_if_has_all_names(kernel_names, section_names))
+        if is_all_true(have, self.group):
             return
         gathered = all_gather_object((section_names, kernel_names), self.group)
         for name in itertools.chain.from_iterable(s for s, _ in gathered):

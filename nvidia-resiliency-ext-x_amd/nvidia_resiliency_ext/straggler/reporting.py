@@ -137,6 +137,8 @@ class ReportGenerator:
         self._hist_k = _History()
         self._hist_s = _History()
         self.name_mapper = NameMapper(pg=pg)
+        self._knames: Tuple[str, ...] = ()
+        self._kcache = None  # (kernel names, their ids, their history slots) of the last report
         self.rank_to_node: Dict[int, str] = collections.defaultdict(lambda: '<unk>')
         self._device: Optional[torch.device] = None
 
@@ -173,13 +175,15 @@ class ReportGenerator:
             keep = np.fromiter(("ncclDev" not in n for n in kernel_summaries.names), dtype=bool,
                                count=len(kernel_summaries))
             return kernel_summaries if keep.all() else kernel_summaries.select(keep)
+        if "ncclDev" not in "\0".join(kernel_summaries):  # (one search instead of one per name)
+            return dict(kernel_summaries)  # (a new mapping, as the comprehension makes)
         return {k: v for k, v in kernel_summaries.items() if "ncclDev" not in k}
 
     # ------------------------------------------------------------------ device scoring
     def _score_local(self, section_summaries, kernel_summaries):
         """Individual / relative GPU and section scores of this rank, on the device."""
         dev = self._dev()
-        knames = list(kernel_summaries.keys())
+        knames = self._knames
         snames = list(section_summaries.keys())
         K, S = len(knames), len(snames)
         kmed, kavg, knum = columns_of(kernel_summaries)
@@ -188,11 +192,17 @@ class ReportGenerator:
         rel, ind = self.is_computing_rel_scores, self.is_computing_indiv_scores
         nk = self.name_mapper.kernel_counter if rel else 0
         nsec = self.name_mapper.section_counter if rel else 0
-        kid = (np.fromiter((self.name_mapper.kernel_name_to_id[n] for n in knames), np.int32, K)
+        # the kernels' ids and history slots never change once assigned: a report over the same
+        # kernel names as the previous one (the usual case) reuses them
+        cache = self._kcache if self._kcache is not None and self._kcache[0] == knames else None
+        kid = (cache[1] if cache is not None else
+               np.fromiter((self.name_mapper.kernel_name_to_id[n] for n in knames), np.int32, K)
                if rel else np.zeros(0, np.int32))
         sid = (np.fromiter((nk + self.name_mapper.section_name_to_id[n] for n in snames),
                            np.int32, S) if rel else np.zeros(0, np.int32))
-        kslot = self._hist_k.slots_for(knames, dev) if ind else np.zeros(0, np.int32)
+        kslot = (cache[2] if cache is not None and self._hist_k.values is not None else
+                 self._hist_k.slots_for(knames, dev) if ind else np.zeros(0, np.int32))
+        self._kcache = (knames, kid, kslot)
         sslot = self._hist_s.slots_for(snames, dev) if ind else np.zeros(0, np.int32)
 
         # one host->device transfer of every input column
@@ -305,10 +315,13 @@ class ReportGenerator:
         self.world_size = dist_utils.get_world_size(self.group)
         self.rank = dist_utils.get_rank(self.group)
         kernel_summaries = self._filter_out_nccl_kernels(kernel_summaries)
+        self._knames = tuple(kernel_summaries.keys())
         self._maybe_gather_rank_to_node()
         if self.is_computing_rel_scores or self.gather_on_rank0:
-            self.name_mapper.gather_and_assign_ids(kernel_names=list(kernel_summaries.keys()),
-                                                   section_names=list(section_summaries.keys()))
+            known = self._kcache is not None and self._kcache[0] == self._knames
+            self.name_mapper.gather_and_assign_ids(kernel_names=list(self._knames),
+                                                   section_names=list(section_summaries.keys()),
+                                                   kernels_known=known)
         gi, si, gr, sr = self._score_local(section_summaries, kernel_summaries)
 
         res_gi: Mapping[int, float] = {}
