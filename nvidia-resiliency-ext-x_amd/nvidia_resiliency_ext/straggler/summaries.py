@@ -9,6 +9,7 @@ caller indexes it.  Values are the float32 statistics widened exactly to Python 
 """
 from __future__ import annotations
 
+import operator
 from typing import Dict, Iterator, List, Mapping, Sequence
 
 import numpy as np
@@ -62,9 +63,12 @@ def columns_of(summaries: Mapping[str, Mapping]) -> tuple:
     if isinstance(summaries, KernelSummaries):
         return summaries.columns()
     n = len(summaries)
-    MED, AVG, NUM = Statistic.MED, Statistic.AVG, Statistic.NUM  # (enum attribute lookups are slow)
     vals = summaries.values()
-    med = np.fromiter((s[MED] for s in vals), np.float64, n)
-    avg = np.fromiter((s[AVG] for s in vals), np.float64, n)
-    num = np.fromiter((s[NUM] for s in vals), np.int64, n)
-    return med, avg, num
+    # C-level item getters over the values (no Python frame per summary)
+    return (np.fromiter(map(_GET_MED, vals), np.float64, n),
+            np.fromiter(map(_GET_AVG, vals), np.float64, n),
+            np.fromiter(map(_GET_NUM, vals), np.int64, n))
+
+
+_GET_MED, _GET_AVG, _GET_NUM = (operator.itemgetter(k) for k in (Statistic.MED, Statistic.AVG,
+                                                                  Statistic.NUM))
