@@ -56,7 +56,12 @@ void q_intercept(const void* pkts, uint64_t n, uint64_t, void* data,
     const auto* in = static_cast<const hsa_kernel_dispatch_packet_t*>(pkts);
     uint64_t nk = 0;
     for (uint64_t i = 0; i < n; ++i) nk += packet_type(in[i].header) == HSA_PACKET_TYPE_KERNEL_DISPATCH;
-    if (nk == 0 || t_mark.depth > 0) {  // t_mark: a report of ours runs on this thread -- not captured
+    // t_mark: a report of ours runs on this thread -- not captured.  This needs the handler on the
+    // launching thread: HIP's direct dispatch (AMD_DIRECT_DISPATCH=0 selects callback delivery at
+    // configuration, capture.cpp) and a queue with room for the packets -- ROCr defers the handler
+    // of a batch that does not fit the wrapped queue.  The Detector synchronizes before it reports
+    // (straggler.py:234-235 in the reference), so its report kernels meet drained queues.
+    if (nk == 0 || t_mark.depth > 0) {
         if (t_mark.depth > 0) c.n_own.fetch_add(nk, std::memory_order_relaxed);
         writer(pkts, n);
         return;
