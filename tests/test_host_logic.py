@@ -156,3 +156,47 @@ def test_sync_mode_switch():
     finally:
         batch.set_sync_mode(prev)
     assert batch.sync_mode() == prev
+
+
+def test_summary_columns_and_nccl_filter():
+    """Host side of a report on the reference's {name: {Statistic: value}} summaries: the columns
+    read for scoring, and the ncclDev filter (reporting.py:330-336) returning a new mapping in
+    the caller's order, with or without names to drop."""
+    import pickle
+
+    import numpy as np
+
+    from nvidia_resiliency_ext.straggler import Statistic as S
+    from nvidia_resiliency_ext.straggler.reporting import ReportGenerator
+    from nvidia_resiliency_ext.straggler.summaries import columns_of
+
+    kk = {f"k{i}": {S.MIN: 0.5, S.MAX: 9.0, S.MED: 1.0 + i, S.AVG: 2.0 + i, S.STD: 0.0, S.NUM: 3 + i}
+          for i in range(5)}
+    med, avg, num = columns_of(kk)
+    assert med.dtype == np.float64 and avg.dtype == np.float64 and num.dtype == np.int64
+    assert med.tolist() == [1.0, 2.0, 3.0, 4.0, 5.0] and num.tolist() == [3, 4, 5, 6, 7]
+    assert [len(c) for c in columns_of({})] == [0, 0, 0]
+    out = ReportGenerator._filter_out_nccl_kernels(kk)
+    assert out == kk and out is not kk and list(out) == list(kk)
+    kk2 = dict(kk)
+    kk2["ncclDevKernel_AllReduce_blk_256_1_1_grid_1_1_1"] = kk["k0"]
+    kk2["k9"] = kk["k1"]
+    out2 = ReportGenerator._filter_out_nccl_kernels(kk2)
+    assert list(out2) == ["k0", "k1", "k2", "k3", "k4", "k9"]
+    # Statistic keys: identity hash, same dict semantics, survive pickling (all_gather_object)
+    d = pickle.loads(pickle.dumps({S.MED: 1.5, S.NUM: 2}))
+    assert d[S.MED] == 1.5 and d[S.NUM] == 2 and hash(S.AVG) == object.__hash__(S.AVG)
+
+
+def test_name_mapper_known_kernels_still_assigns_new_sections():
+    """gather_and_assign_ids(kernels_known=True) -- the ReportGenerator's shortcut while the kernel
+    names repeat -- skips only the kernel lookups: a new section still gets its id."""
+    from nvidia_resiliency_ext.straggler.name_mapper import NameMapper
+
+    nm = NameMapper()
+    nm.gather_and_assign_ids(["ka", "kb"], ["s0"])
+    assert nm.kernel_name_to_id == {"ka": 0, "kb": 1} and nm.section_name_to_id == {"s0": 0}
+    nm.gather_and_assign_ids(["ka", "kb"], ["s0", "s1"], kernels_known=True)
+    assert nm.section_name_to_id == {"s0": 0, "s1": 1} and nm.kernel_counter == 2
+    nm.gather_and_assign_ids(["ka", "kb", "kc"], ["s1"])
+    assert nm.kernel_name_to_id["kc"] == 2
