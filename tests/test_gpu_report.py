@@ -255,3 +255,43 @@ def test_golden_scenarios(scname, stats_source):
     if sc["gather"] or "relative_perf_scores" in sc["scores"]:
         assert res[0]["mapper"]["kernel"] == fx["name_mapper"]["kernel"]
         assert res[0]["mapper"]["section"] == fx["name_mapper"]["section"]
+
+
+def test_dropin_2048_kernels_with_name_churn_matches_restatement():
+    """One rank's ReportGenerator at the bench's drop-in size (2,048 kernels, 3 sections) over
+    reports whose kernel set repeats (the id / history-slot cache), shrinks, grows and gains
+    ncclDev names -- every report's GPU and section scores against the CPU restatement of the
+    reference (oracle/oracle_report.py), within the 1e-6 bar; individual history included."""
+    import oracle_report as OR
+
+    from nvidia_resiliency_ext.straggler import Statistic as S
+    from nvidia_resiliency_ext.straggler import reporting, synth
+
+    rng = np.random.default_rng(11)
+    names = synth.kernel_names(2048 + 64)
+    base = {n: (int(rng.integers(1, 8193)), float(np.float32(rng.uniform(2.0, 2000.0))))
+            for n in names}
+    sets = [names[:2048], names[:2048], names[100:2048], names[100:2048] + names[2048:2098],
+            names[100:2048] + names[2048:2098],
+            names[:2048] + ["ncclDevKernel_AllReduce_blk_256_1_1_grid_8_1_1"]]
+    base["ncclDevKernel_AllReduce_blk_256_1_1_grid_8_1_1"] = (5, 3.0)
+    scores = ["relative_perf_scores", "individual_perf_scores"]
+    gen = reporting.ReportGenerator(scores_to_compute=scores, gather_on_rank0=False)
+    sim = OR.SimWorld(1, scores, gather_on_rank0=False)
+    for i, ks in enumerate(sets):
+        j = 1.0 + 0.03 * ((i * 5) % 7)
+        kk = {n: {S.MIN: 0.1, S.MAX: 1e4, S.MED: float(np.float32(base[n][1] * j)),
+                  S.AVG: float(np.float32(base[n][1] * j * 1.01)), S.STD: 0.5, S.NUM: base[n][0]}
+              for n in ks}
+        ss = {f"section_{s}": {S.MIN: 1.0, S.MAX: 9.0, S.MED: 3.0 + s * j, S.AVG: 3.0, S.STD: 0.1,
+                               S.NUM: 10} for s in range(3)}
+        str_k = {n: {OR.MED: v[S.MED], OR.AVG: v[S.AVG], OR.NUM: v[S.NUM]} for n, v in kk.items()}
+        str_s = {n: {OR.MED: v[S.MED], OR.AVG: v[S.AVG], OR.NUM: v[S.NUM]} for n, v in ss.items()}
+        got = gen.generate_report(ss, kk)
+        want = sim.generate_report([str_s], [str_k])[0]
+        for f in ("gpu_relative_perf_scores", "gpu_individual_perf_scores"):
+            assert math.isclose(getattr(got, f)[0], want[f][0], rel_tol=1e-6), (i, f)
+        for f in ("section_relative_perf_scores", "section_individual_perf_scores"):
+            for sec, per_rank in want[f].items():
+                assert math.isclose(getattr(got, f)[sec][0], per_rank[0], rel_tol=1e-6), (i, f, sec)
+        assert "ncclDevKernel_AllReduce_blk_256_1_1_grid_8_1_1" not in got.local_kernel_summaries
